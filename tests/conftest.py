@@ -1,0 +1,41 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json"]
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+_cache = {}
+
+
+def load_fixture(name):
+    if name not in _cache:
+        with open(os.path.join(GOLDEN, name)) as f:
+            _cache[name] = json.load(f)
+    return _cache[name]
+
+
+def hx(s):
+    """Parse a fixture big-int string ('0x..' or '-0x..')."""
+    return -int(s[1:], 16) if s.startswith("-") else int(s, 16)
+
+
+def fl(s):
+    return float.fromhex(s)
+
+
+@pytest.fixture(params=FIXTURES)
+def golden(request):
+    return load_fixture(request.param)
