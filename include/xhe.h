@@ -1,0 +1,83 @@
+/* xhe — MI355X (gfx950) Paillier hot path, C ABI.
+ *
+ * Drop-in boundary for XFL's python/common/crypto/paillier (reference paths
+ * below are relative to /root/reference/python). Every entry point takes plain
+ * pointers and sizes; "_dev" pointers are device (HBM) buffers owned by the
+ * caller, "_host" entry points take host buffers and do the H2D/D2H copies.
+ * Big integers are little-endian arrays of 32-bit words:
+ *   n: nw = key_bits/32 words, ciphertexts (mod n^2): n2w = 2*nw words,
+ *   randomness a (DJN) / r (non-DJN): rand_words words per element.
+ * Return value: 0 on success, negative XHE_E* on failure; xhe_last_error()
+ * gives the thread-local message. A key handle is immutable after creation
+ * and may be shared between threads; calls on distinct streams are reentrant.
+ */
+#ifndef XHE_H
+#define XHE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XHE_OK 0
+#define XHE_EINVAL -1     /* bad argument (TypeError/ValueError side)          */
+#define XHE_EOVERFLOW -2  /* value out of the encodable/decodable range        */
+#define XHE_EHIP -3       /* HIP runtime error                                  */
+#define XHE_ENOINV -4     /* no modular inverse (ZeroDivisionError)             */
+#define XHE_ENOTSUP -5    /* mode not built for this key size                   */
+
+typedef struct xhe_key xhe_key;
+
+/* Key material -> device key handle with all per-key precomputes
+ * (PaillierContext.init, context.py:28-71) and, for a DJN private key, the
+ * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win_bits rows per window).
+ * p_words/q_words NULL => public key (n only). h_pow_n_words NULL => DJN off.
+ * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in {4, 8} (0 = default). */
+int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
+                   const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
+void xhe_key_destroy(xhe_key* key);
+/* nw, n2w, rand_words (32-bit words per randomness draw), rand_bits
+ * (DJN: bitlen(n)//2 = log2 djn_exp_bound; non-DJN: bitlen(n)), flags bit0
+ * private, bit1 djn. */
+int xhe_key_info(const xhe_key* key, int* key_bits, int* nw, int* n2w, int* rand_words, int* rand_bits, int* flags);
+
+/* PaillierEncoder.cal_exponent + encode_single over float64 (encoder.py:29-54,
+ * paillier.py:279-282). precision < 0 => None (frexp exponent), else
+ * e = -ceil(log2(10)*precision). has_max => e = min(e, max_exponent).
+ * Per element: m (nw words), exponent, status (0, 1 = OverflowError, 2 = ValueError). */
+int xhe_encode_f64(const xhe_key* key, const double* x_dev, int64_t count, int precision, int has_max,
+                   int max_exponent, uint32_t* m_dev, int32_t* exp_dev, int32_t* status_dev, void* stream);
+
+/* Obfuscation randomness from a ChaCha20 stream keyed by seed32 (32 bytes) and
+ * nonce: DJN a in [1, djn_exp_bound) (paillier.py:195,211) or non-DJN r in
+ * [1, n) (paillier.py:215,229). Replaces secrets.SystemRandom().randrange. */
+int xhe_rand(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_t count, uint32_t* rand_dev,
+             int32_t* status_dev, void* stream);
+
+/* Paillier._encrypt_single + PaillierCiphertext.obfuscate (paillier.py:273-287,
+ * 189-232): ct = (1 + n*m) * X mod n^2 with X from rand (NULL = no obfuscation). */
+int xhe_encrypt(const xhe_key* key, const uint32_t* m_dev, const uint32_t* rand_dev, int64_t count,
+                uint32_t* ct_dev, void* stream);
+
+/* Paillier._decrypt_single arithmetic (paillier.py:341-366): ct -> encoded m. */
+int xhe_decrypt(const xhe_key* key, const uint32_t* ct_dev, int64_t count, uint32_t* m_dev, void* stream);
+
+/* PaillierEncoder.decode_single + astype(np.float32) (encoder.py:56-64,
+ * paillier.py:396-398): f64 = value before the float32 cast, f32 = result;
+ * status 1 = OverflowError (decode range), 3 = OverflowError (mpz->float). */
+int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev, int64_t count, double* f64_dev,
+               float* f32_dev, int32_t* status_dev, void* stream);
+
+/* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
+int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct);
+int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint32_t* m);
+
+int xhe_device_count(void);
+int xhe_synchronize(void* stream);
+const char* xhe_last_error(void);
+const char* xhe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,165 @@
+"""ctypes binding of the xhe C ABI (include/xhe.h) built from xfl_amd/csrc.
+
+The shared library is built in-tree (xfl_amd/lib/libxhe.so) by
+`__graft_entry__.build()` / `python -m xfl_amd.build`. There is no CPU
+fallback: if the library or a GPU is missing, every entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libxhe.so")
+
+XHE_OK = 0
+XHE_EINVAL = -1
+XHE_EOVERFLOW = -2
+XHE_EHIP = -3
+XHE_ENOINV = -4
+XHE_ENOTSUP = -5
+
+_lib = None
+_lock = threading.Lock()
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); every symbol declared in include/xhe.h
+SIGNATURES = {
+    "xhe_key_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u32p, _u32p, _u32p, _u32p, ctypes.c_int,
+                                      ctypes.POINTER(_vp)]),
+    "xhe_key_destroy": (None, [_vp]),
+    "xhe_key_info": (ctypes.c_int, [_vp] + [ctypes.POINTER(ctypes.c_int)] * 6),
+    "xhe_encode_f64": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      _vp, _vp, _vp, _vp]),
+    "xhe_rand": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64, _vp, _vp, _vp]),
+    "xhe_encrypt": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp]),
+    "xhe_decrypt": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp]),
+    "xhe_decode": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
+    "xhe_encrypt_host": (ctypes.c_int, [_vp, _u32p, _u32p, ctypes.c_int64, _u32p]),
+    "xhe_decrypt_host": (ctypes.c_int, [_vp, _u32p, ctypes.c_int64, _u32p]),
+    "xhe_device_count": (ctypes.c_int, []),
+    "xhe_synchronize": (ctypes.c_int, [_vp]),
+    "xhe_last_error": (ctypes.c_char_p, []),
+    "xhe_version": (ctypes.c_char_p, []),
+}
+
+
+class XheError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libxhe.so once; raise loudly if it is missing (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise XheError(f"xfl_amd native library not built: {LIB_PATH} missing "
+                               "(run __graft_entry__.build())")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc == XHE_OK:
+        return
+    msg = lib().xhe_last_error().decode(errors="replace")
+    if rc == XHE_EOVERFLOW:
+        raise OverflowError(msg)
+    if rc == XHE_ENOINV:
+        raise ZeroDivisionError(msg)
+    if rc == XHE_EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    raise XheError(f"{what} failed ({rc}): {msg}")
+
+
+# ------------------------------------------------------------ int <-> words
+def int_to_words(x, nw):
+    return np.frombuffer(int(x).to_bytes(4 * nw, "little"), dtype="<u4").copy()
+
+
+def ints_to_words(xs, nw):
+    out = np.empty((len(xs), nw), dtype=np.uint32)
+    nb = 4 * nw
+    buf = bytearray(nb * len(xs))
+    for i, x in enumerate(xs):
+        buf[i * nb:(i + 1) * nb] = int(x).to_bytes(nb, "little")
+    out[:] = np.frombuffer(bytes(buf), dtype="<u4").reshape(len(xs), nw)
+    return out
+
+
+def words_to_ints(w):
+    w = np.ascontiguousarray(w, dtype="<u4")
+    if w.ndim == 1:
+        return int.from_bytes(w.tobytes(), "little")
+    nb = w.shape[1] * 4
+    raw = w.tobytes()
+    return [int.from_bytes(raw[i * nb:(i + 1) * nb], "little") for i in range(w.shape[0])]
+
+
+def ptr(a):
+    return a.ctypes.data_as(_u32p)
+
+
+class DeviceKey:
+    """Owns one xhe_key handle (device-resident key constants and tables)."""
+
+    def __init__(self, key_bits, n, p=None, q=None, h_pow_n=None, device=0, win_bits=0):
+        L = lib()
+        self.key_bits = key_bits
+        self.nw = key_bits // 32
+        self.n2w = 2 * self.nw
+        nw_ = int_to_words(n, self.nw)
+        pw = int_to_words(p, self.nw // 2) if p is not None else None
+        qw = int_to_words(q, self.nw // 2) if q is not None else None
+        hw = int_to_words(h_pow_n, self.n2w) if h_pow_n else None
+        h = _vp()
+        rc = L.xhe_key_create(device, key_bits, ptr(nw_), ptr(pw) if pw is not None else None,
+                              ptr(qw) if qw is not None else None, ptr(hw) if hw is not None else None,
+                              win_bits, ctypes.byref(h))
+        check(rc, "xhe_key_create")
+        self.handle = h
+        vals = [ctypes.c_int() for _ in range(6)]
+        check(L.xhe_key_info(h, *[ctypes.byref(v) for v in vals]), "xhe_key_info")
+        _, _, _, self.rand_words, self.rand_bits, flags = [v.value for v in vals]
+        self.private = bool(flags & 1)
+        self.djn = bool(flags & 2)
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib is not None:
+            _lib.xhe_key_destroy(h)
+            self.handle = None
+
+    # host-buffer paths (used by the drop-in API)
+    def encrypt_words(self, m_words, rand_words):
+        m_words = np.ascontiguousarray(m_words, dtype=np.uint32)
+        count = m_words.shape[0]
+        out = np.empty((count, self.n2w), dtype=np.uint32)
+        if count == 0:
+            return out
+        r = None if rand_words is None else np.ascontiguousarray(rand_words, dtype=np.uint32)
+        check(lib().xhe_encrypt_host(self.handle, ptr(m_words), ptr(r) if r is not None else None, count,
+                                     ptr(out)), "xhe_encrypt")
+        return out
+
+    def decrypt_words(self, c_words):
+        c_words = np.ascontiguousarray(c_words, dtype=np.uint32)
+        count = c_words.shape[0]
+        out = np.empty((count, self.nw), dtype=np.uint32)
+        if count == 0:
+            return out
+        check(lib().xhe_decrypt_host(self.handle, ptr(c_words), count, ptr(out)), "xhe_decrypt")
+        return out

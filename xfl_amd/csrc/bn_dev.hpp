@@ -1,0 +1,422 @@
+// Device multi-precision Montgomery arithmetic for gfx950 (CDNA4).
+//
+// Representation: a residue mod M is S limbs of W bits (W = 27/28) held one
+// limb per 32-bit VGPR. A group of TPI consecutive lanes (TPI in {1,2,4})
+// owns one residue, lane g holding limbs [g*L, (g+1)*L), L = S/TPI.
+//
+// The Montgomery product is operand scanning with LAZY carries: the running
+// sum lives in L 64-bit accumulators per lane, every limb product is a single
+// v_mad_u64_u32 (32x32+64 -> 64) and no carry is propagated inside the loop.
+// With W-bit limbs each accumulator collects at most 2S products of < 2^(2W)
+// along its anti-diagonal, so 2S * 2^(2W) < 2^64 is the only constraint
+// (static_assert below). The divide-by-2^W shift is folded into the mad
+// destinations (T[j-1] = T[j] + a_i*b[j] + m*N[j]) and across lanes it is a
+// single DPP quad_perm move, so the inner loop is 2L mads + O(1) per limb of a.
+//
+// R = 2^(W*S) >= 16*M for every modulus we instantiate, so products of inputs
+// below 2M (and up to ~R/M times larger for one operand) stay below 2M and no
+// conditional subtraction is needed between products ("almost Montgomery").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xhe {
+
+#define XHE_DEV __device__ __forceinline__
+
+// d = a*b + c with one v_mad_u64_u32. Inline asm keeps a and b 32-bit: the
+// C form (uint64_t)a*b + c makes the compiler hold every limb as a
+// zero-extended 64-bit register pair, doubling the resident operand.
+XHE_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "vcc");
+  return c;
+}
+// same with a wave-uniform b (SGPR operand)
+XHE_DEV uint64_t mad64s(uint32_t a, uint32_t b_uniform, uint64_t c) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "s"(b_uniform) : "vcc");
+  return c;
+}
+
+// ------------------------------------------------------------ lane groups
+template <int TPI>
+struct Grp {
+  static XHE_DEV int g() { return TPI == 1 ? 0 : (int)(threadIdx.x & (TPI - 1)); }
+
+  // value held by lane 0 of the group
+  static XHE_DEV uint32_t bcast0(uint32_t v) {
+    if constexpr (TPI == 1) return v;
+    else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x00, 0xF, 0xF, false);
+  }
+  // value held by the last lane of the group
+  static XHE_DEV uint32_t bcast_last(uint32_t v) {
+    if constexpr (TPI == 1) return v;
+    else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF5, 0xF, 0xF, false);
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false);
+  }
+  // value held by lane g+1 (0 for the last lane)
+  static XHE_DEV uint32_t from_next(uint32_t v) {
+    if constexpr (TPI == 1) return 0u;
+    else {
+      uint32_t r;
+      if constexpr (TPI == 2) r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF5, 0xF, 0xF, false);
+      else r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF9, 0xF, 0xF, false);
+      return g() == TPI - 1 ? 0u : r;
+    }
+  }
+  // value held by lane g-1 (0 for lane 0)
+  static XHE_DEV uint32_t from_prev(uint32_t v) {
+    if constexpr (TPI == 1) return 0u;
+    else {
+      uint32_t r;
+      if constexpr (TPI == 2) r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);
+      else r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x90, 0xF, 0xF, false);
+      return g() == 0 ? 0u : r;
+    }
+  }
+  static XHE_DEV uint64_t from_next64(uint64_t v) {
+    return (uint64_t)from_next((uint32_t)v) | ((uint64_t)from_next((uint32_t)(v >> 32)) << 32);
+  }
+  static XHE_DEV uint64_t from_prev64(uint64_t v) {
+    return (uint64_t)from_prev((uint32_t)v) | ((uint64_t)from_prev((uint32_t)(v >> 32)) << 32);
+  }
+};
+
+// ------------------------------------------------------ operand-a sources
+// a_i is uniform inside a lane group. load4(i) returns limbs i..i+3 (rows are
+// padded to a multiple of 4 words, so i+3 may touch padding).
+struct ARow {  // one contiguous row of W-limbs (16-byte aligned)
+  const uint32_t* __restrict__ p;
+  XHE_DEV uint4 load4(int i) const { return *reinterpret_cast<const uint4*>(p + i); }
+};
+struct AStrided {  // interleaved workspace row: limb i at p[i*stride]
+  const uint32_t* p;
+  int stride;
+  XHE_DEV uint4 load4(int i) const {
+    const uint32_t* q = p + (size_t)i * stride;
+    return make_uint4(q[0], q[stride], q[2 * (size_t)stride], q[3 * (size_t)stride]);
+  }
+};
+struct ALds {  // group row in LDS: limb i at p[i]
+  const uint32_t* p;
+  XHE_DEV uint4 load4(int i) const { return make_uint4(p[i], p[i + 1], p[i + 2], p[i + 3]); }
+};
+struct AOne {  // the integer 1 (Montgomery reduction of b)
+  XHE_DEV uint4 load4(int i) const { return make_uint4(i == 0 ? 1u : 0u, 0u, 0u, 0u); }
+};
+struct AZero {
+  XHE_DEV uint4 load4(int) const { return make_uint4(0u, 0u, 0u, 0u); }
+};
+
+XHE_DEV uint32_t comp4(const uint4& v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
+
+// Pack `nlimbs` W-bit limbs (one per word, limb i at p[i*stride]) into
+// nwords little-endian 32-bit words. Executed by lane `g` of a TPI group for
+// words k = g, g+TPI, ...  (limbs beyond nlimbs read as zero).
+template <int W, int TPI>
+XHE_DEV void pack_words_(const uint32_t* p, int stride, int nlimbs, uint32_t* __restrict__ out, int nwords) {
+  const int g = Grp<TPI>::g();
+  for (int k = g; k < nwords; k += TPI) {
+    int bit = 32 * k;
+    int j = bit / W, sh = bit - j * W;
+    uint64_t v = 0;
+    if (j < nlimbs) v |= (uint64_t)p[(size_t)j * stride];
+    if (j + 1 < nlimbs) v |= (uint64_t)p[(size_t)(j + 1) * stride] << W;
+    if (j + 2 < nlimbs) v |= (uint64_t)p[(size_t)(j + 2) * stride] << (2 * W);
+    out[k] = (uint32_t)(v >> sh);
+  }
+}
+
+// Workgroup-scope fence: makes this wave's global/LDS writes visible to the
+// other lanes of the same wave before they read them.
+XHE_DEV void wave_sync_mem_() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// --------------------------------------------------------------- modulus
+template <int S_, int W_, int TPI_>
+struct Mont {
+  static constexpr int S = S_, W = W_, TPI = TPI_, L = S_ / TPI_;
+  static constexpr int S4 = (S_ + 3) & ~3;  // padded row length (words)
+  static constexpr uint32_t MASK = (1u << W_) - 1u;
+  static_assert(S_ % TPI_ == 0, "S must be a multiple of TPI");
+  static_assert(W_ <= 30, "W too large");
+  // lazy-carry bound: 2S products of (2^W-1)^2 plus a W-bit carry-in per column
+  static_assert((double)(2 * S_ + 2) * (double)(1ull << W_) * (double)(1ull << W_) < 18446744073709551616.0,
+                "accumulator would overflow");
+  using G = Grp<TPI_>;
+
+  const uint32_t* __restrict__ N;  // S limbs (uniform)
+  uint32_t n0inv;                  // -N^-1 mod 2^W
+  uint32_t nl[TPI_ == 1 ? 1 : L];  // this lane's modulus limbs (TPI > 1)
+
+  XHE_DEV void init(const uint32_t* Np, uint32_t ninv) {
+    // N + opaque 0: same provenance (keeps noalias, so limb loads stay scalar
+    // s_loads) but the loads cannot be hoisted above this point. Limbs are
+    // then held in SGPRs only while this Mont object is in use.
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    N = Np + z;
+    n0inv = ninv;
+    if constexpr (TPI > 1) {
+      const int g = G::g();
+#pragma unroll
+      for (int j = 0; j < L; ++j) nl[j] = Np[g * L + j];
+    }
+  }
+  XHE_DEV const uint32_t* np() const { return N; }
+  XHE_DEV uint32_t nj(const uint32_t* Np, int j) const {
+    if constexpr (TPI == 1) return Np[j];
+    else return nl[j];
+  }
+  // m * N[j] + c
+  XHE_DEV uint64_t madN(const uint32_t* Np, uint32_t m, int j, uint64_t c) const {
+    if constexpr (TPI == 1) return mad64s(m, Np[j], c);
+    else return mad64(m, nl[j], c);
+  }
+
+  // One column of the product: T <- (T + a_i*b + m*N) / 2^W
+  XHE_DEV void step(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, bool lead) const {
+    uint64_t x0 = mad64(ai, b[0], T[0]);
+    uint32_t m = ((uint32_t)x0 * n0inv) & MASK;
+    m = G::bcast0(m);
+    x0 = madN(Np, m, 0, x0);
+#pragma unroll
+    for (int j = 1; j < L; ++j) T[j - 1] = madN(Np, m, j, mad64(ai, b[j], T[j]));
+    T[L - 1] = G::from_next64(x0);
+    T[0] += lead ? (x0 >> W) : 0ull;
+  }
+
+  // Carry-normalise the accumulators into W-bit limbs.
+  XHE_DEV void normalize(const uint64_t (&T)[L], uint32_t (&b)[L]) const {
+    // sched_barrier per limb keeps the scheduler from hoisting every 64-bit
+    // partial sum ahead of its mask (which doubles the live registers).
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      uint64_t x = T[j] + c;
+      b[j] = (uint32_t)x & MASK;
+      c = x >> W;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (TPI > 1) {
+#pragma unroll
+      for (int r = 1; r < TPI; ++r) {
+        uint64_t cin = G::from_prev64(c);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          uint64_t x = (uint64_t)b[j] + cin;
+          b[j] = (uint32_t)x & MASK;
+          cin = x >> W;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        c = cin;
+      }
+    }
+  }
+
+  // b <- a * b * R^-1 mod N  (result < 2N for inputs in range)
+  template <class A>
+  XHE_DEV void mul(uint32_t (&b)[L], const A& a) const {
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = 0;
+    run<A>(T, b, a);
+    normalize(T, b);
+  }
+
+  template <class A>
+  XHE_DEV void run(uint64_t (&T)[L], const uint32_t (&b)[L], const A& a) const {
+    const bool lead = G::g() == 0;
+    const uint32_t* Np = np();
+    uint4 cur = a.load4(0);
+    int i = 0;
+    for (; i + 4 <= S; i += 4) {
+      uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
+      __builtin_amdgcn_sched_barrier(0);
+      step(Np, T, b, cur.x, lead);
+      __builtin_amdgcn_sched_barrier(0);
+      step(Np, T, b, cur.y, lead);
+      __builtin_amdgcn_sched_barrier(0);
+      step(Np, T, b, cur.z, lead);
+      __builtin_amdgcn_sched_barrier(0);
+      step(Np, T, b, cur.w, lead);
+      __builtin_amdgcn_sched_barrier(0);
+      cur = nxt;
+    }
+#pragma unroll
+    for (int r = 0; r < (S & 3); ++r) step(Np, T, b, comp4(cur, r), lead);
+  }
+
+  // Montgomery reduction of a double-length value: lo = limbs [0,S) in b,
+  // hi limbs [S, 2S) supplied by `hi` (uniform a-source). Returns
+  // (hi*2^(WS) + lo) * R^-1 mod N in b (< 2N when the input < R*N).
+  template <class A>
+  XHE_DEV void redc_wide(uint32_t (&b)[L], const A& hi) const {
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = b[j];
+    const bool lead = G::g() == 0;
+    const bool last = G::g() == TPI - 1;
+    const uint32_t* Np = np();
+    for (int i0 = 0; i0 < S4; i0 += 4) {
+      uint4 h4 = hi.load4(i0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (i0 + r < S) {
+          uint64_t x0 = T[0];
+          uint32_t m = ((uint32_t)x0 * n0inv) & MASK;
+          m = G::bcast0(m);
+          x0 = madN(Np, m, 0, x0);
+#pragma unroll
+          for (int j = 1; j < L; ++j) T[j - 1] = madN(Np, m, j, T[j]);
+          uint64_t up = G::from_next64(x0);
+          T[L - 1] = last ? (uint64_t)comp4(h4, r) : up;
+          T[0] += lead ? (x0 >> W) : 0ull;
+        }
+      }
+    }
+    normalize(T, b);
+  }
+
+  // b in [0, 2N) -> [0, N)
+  XHE_DEV void reduce_once(uint32_t (&b)[L]) const {
+    uint32_t d[L];
+    uint32_t br = 0;
+    const uint32_t* Np = np();
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      int64_t x = (int64_t)b[j] - (int64_t)nj(Np, j) - (int64_t)br;
+      br = x < 0 ? 1u : 0u;
+      d[j] = (uint32_t)(x + ((int64_t)br << W));
+    }
+    if constexpr (TPI > 1) {
+      // each round moves borrows one lane up; the top lane's total borrow is
+      // its local borrow plus every borrow it generates while absorbing them
+      uint32_t total = br;
+#pragma unroll
+      for (int r = 1; r < TPI; ++r) {
+        uint32_t bin = G::from_prev(br);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          int64_t x = (int64_t)d[j] - (int64_t)bin;
+          bin = x < 0 ? 1u : 0u;
+          d[j] = (uint32_t)(x + ((int64_t)bin << W));
+        }
+        br = bin;
+        total |= bin;
+      }
+      br = G::bcast_last(total);
+    }
+    if (!br) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) b[j] = d[j];
+    }
+  }
+
+  // b <- b + addend - subtrahend (all as W-limb values, result must be >= 0)
+  // addend limbs from a group row (ARow-like pointer), subtrahend from `sub`.
+  XHE_DEV void add_sub_rows(uint32_t (&b)[L], const uint32_t* add, const uint32_t* subp, int sub_stride) const {
+    const int g = G::g();
+    int64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      int64_t x = (int64_t)b[j] + (int64_t)add[g * L + j] - (int64_t)subp[(size_t)(g * L + j) * sub_stride] + c;
+      c = x >> W;  // arithmetic shift: floor division
+      b[j] = (uint32_t)(x & MASK);
+    }
+    if constexpr (TPI > 1) {
+#pragma unroll
+      for (int r = 1; r < TPI; ++r) {
+        int64_t cin = (int64_t)G::from_prev64((uint64_t)c);
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          int64_t x = (int64_t)b[j] + cin;
+          cin = x >> W;
+          b[j] = (uint32_t)(x & MASK);
+        }
+        c = cin;
+      }
+    }
+  }
+
+  // b <- b + row (W-limb row, uniform pointer); carries normalised
+  XHE_DEV void add_row(uint32_t (&b)[L], const uint32_t* row) const {
+    const int g = G::g();
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = (uint64_t)b[j] + row[g * L + j];
+    normalize(T, b);
+  }
+
+  // Wide product with addend: out = init + b * a, where a is a uniform row of
+  // S limbs, init an interleaved row of S limbs at ws (stride). The 2S result
+  // limbs are written to the same interleaved row (ws must hold 2*S4 limbs),
+  // then packed into nwords little-endian words at `out`.
+  template <class A>
+  XHE_DEV void wide_mul_add_store(const uint32_t (&b)[L], const A& a, uint32_t* ws, int stride,
+                                  uint32_t* __restrict__ out, int nwords) const {
+    const int g = G::g();
+    const bool lead = g == 0;
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = ws[(size_t)(g * L + j) * stride];
+    wave_sync_mem_();
+    for (int i0 = 0; i0 < S4; i0 += 4) {
+      uint4 a4 = a.load4(i0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (i0 + r < S) {
+          uint32_t ai = comp4(a4, r);
+          uint64_t x0 = mad64(ai, b[0], T[0]);
+          if (lead) ws[(size_t)(i0 + r) * stride] = (uint32_t)x0 & MASK;
+#pragma unroll
+          for (int j = 1; j < L; ++j) T[j - 1] = mad64(ai, b[j], T[j]);
+          T[L - 1] = G::from_next64(x0);
+          T[0] += lead ? (x0 >> W) : 0ull;
+        }
+      }
+    }
+    uint32_t hi[L];
+    normalize(T, hi);
+#pragma unroll
+    for (int j = 0; j < L; ++j) ws[(size_t)(S + g * L + j) * stride] = hi[j];
+    wave_sync_mem_();
+    pack_words_<W, TPI>(ws, stride, 2 * S, out, nwords);
+  }
+
+  // ---------------------------------------------------------------- I/O
+  // Load W-limbs from a little-endian 32-bit word array of nwords words.
+  XHE_DEV void load_words(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      int bit = W * (g * L + j);
+      int k = bit >> 5, sh = bit & 31;
+      uint32_t lo = k < nwords ? w[k] : 0u;
+      uint32_t hi = k + 1 < nwords ? w[k + 1] : 0u;
+      b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
+    }
+  }
+  // Store this lane's limbs one per word into an interleaved row.
+  XHE_DEV void store_strided(const uint32_t (&b)[L], uint32_t* p, int stride) const {
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j) p[(size_t)(g * L + j) * stride] = b[j];
+  }
+  XHE_DEV void load_strided(uint32_t (&b)[L], const uint32_t* p, int stride) const {
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j) b[j] = p[(size_t)(g * L + j) * stride];
+  }
+  XHE_DEV void load_row(uint32_t (&b)[L], const uint32_t* p) const {
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j) b[j] = p[g * L + j];
+  }
+  XHE_DEV void store_row(const uint32_t (&b)[L], uint32_t* p) const {
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j) p[g * L + j] = b[j];
+  }
+};
+
+}  // namespace xhe

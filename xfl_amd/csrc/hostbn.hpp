@@ -1,0 +1,211 @@
+// Host-side multi-precision integers for key setup (runs once per key).
+//
+// Derives the per-key constants of PaillierContext.init
+// (reference python/common/crypto/paillier/context.py:28-71) and the
+// Montgomery constants the device kernels need. Not on the per-element path.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <vector>
+
+namespace xhe {
+
+struct BigU {
+  std::vector<uint32_t> w;  // little-endian 32-bit words, no leading zeros
+
+  BigU() = default;
+  explicit BigU(uint64_t v) {
+    if (v) w.push_back((uint32_t)v);
+    if (v >> 32) w.push_back((uint32_t)(v >> 32));
+  }
+  static BigU from_words(const uint32_t* p, size_t n) {
+    BigU r;
+    r.w.assign(p, p + n);
+    r.trim();
+    return r;
+  }
+  void trim() {
+    while (!w.empty() && w.back() == 0) w.pop_back();
+  }
+  bool is_zero() const { return w.empty(); }
+  size_t bits() const {
+    if (w.empty()) return 0;
+    return 32 * (w.size() - 1) + (32 - __builtin_clz(w.back()));
+  }
+  uint32_t word(size_t i) const { return i < w.size() ? w[i] : 0u; }
+  int bit(size_t i) const { return (int)((word(i >> 5) >> (i & 31)) & 1u); }
+  void to_words(uint32_t* out, size_t n) const {
+    if (w.size() > n) throw std::runtime_error("BigU::to_words: value too large");
+    for (size_t i = 0; i < n; ++i) out[i] = word(i);
+  }
+  // W-bit limbs, S of them (value must fit)
+  std::vector<uint32_t> to_limbs(int W, int S) const {
+    if ((int)bits() > W * S) throw std::runtime_error("BigU::to_limbs: value too large");
+    std::vector<uint32_t> r(S);
+    uint64_t mask = (1ull << W) - 1;
+    for (int j = 0; j < S; ++j) {
+      size_t bitpos = (size_t)W * j;
+      size_t k = bitpos >> 5, sh = bitpos & 31;
+      uint64_t v = (uint64_t)word(k) | ((uint64_t)word(k + 1) << 32);
+      r[j] = (uint32_t)((v >> sh) & mask);
+    }
+    return r;
+  }
+};
+
+inline int cmp(const BigU& a, const BigU& b) {
+  if (a.w.size() != b.w.size()) return a.w.size() < b.w.size() ? -1 : 1;
+  for (size_t i = a.w.size(); i-- > 0;)
+    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
+  return 0;
+}
+
+inline BigU add(const BigU& a, const BigU& b) {
+  BigU r;
+  size_t n = std::max(a.w.size(), b.w.size());
+  r.w.resize(n + 1);
+  uint64_t c = 0;
+  for (size_t i = 0; i < n; ++i) {
+    c += (uint64_t)a.word(i) + b.word(i);
+    r.w[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  r.w[n] = (uint32_t)c;
+  r.trim();
+  return r;
+}
+
+// a - b, requires a >= b
+inline BigU sub(const BigU& a, const BigU& b) {
+  if (cmp(a, b) < 0) throw std::runtime_error("BigU::sub: negative result");
+  BigU r;
+  r.w.resize(a.w.size());
+  int64_t br = 0;
+  for (size_t i = 0; i < a.w.size(); ++i) {
+    int64_t d = (int64_t)a.w[i] - (int64_t)b.word(i) - br;
+    br = d < 0;
+    r.w[i] = (uint32_t)(d + (br << 32));
+  }
+  r.trim();
+  return r;
+}
+
+inline BigU mul(const BigU& a, const BigU& b) {
+  BigU r;
+  if (a.is_zero() || b.is_zero()) return r;
+  r.w.assign(a.w.size() + b.w.size(), 0);
+  for (size_t i = 0; i < a.w.size(); ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; j < b.w.size(); ++j) {
+      c += (uint64_t)a.w[i] * b.w[j] + r.w[i + j];
+      r.w[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    r.w[i + b.w.size()] = (uint32_t)c;
+  }
+  r.trim();
+  return r;
+}
+
+inline BigU shl(const BigU& a, size_t s) {
+  BigU r;
+  if (a.is_zero()) return r;
+  size_t ws = s >> 5, bs = s & 31;
+  r.w.assign(a.w.size() + ws + 1, 0);
+  for (size_t i = 0; i < a.w.size(); ++i) {
+    uint64_t v = (uint64_t)a.w[i] << bs;
+    r.w[i + ws] |= (uint32_t)v;
+    r.w[i + ws + 1] |= (uint32_t)(v >> 32);
+  }
+  r.trim();
+  return r;
+}
+
+inline BigU pow2(size_t s) { return shl(BigU(1), s); }
+
+// q = a / m, r = a % m (binary long division over the quotient bits only)
+inline void divmod(const BigU& a, const BigU& m, BigU* q, BigU* r) {
+  if (m.is_zero()) throw std::runtime_error("BigU::divmod: division by zero");
+  size_t ab = a.bits(), mb = m.bits();
+  BigU quo, rem;
+  if (ab < mb) {
+    if (q) *q = quo;
+    if (r) *r = a;
+    return;
+  }
+  size_t s = ab - mb;
+  // rem = a >> s
+  rem.w.assign(((ab - s) + 31) / 32 + 1, 0);
+  for (size_t i = 0; i < ab - s; ++i)
+    if (a.bit(i + s)) rem.w[i >> 5] |= 1u << (i & 31);
+  rem.trim();
+  quo.w.assign(s / 32 + 1, 0);
+  for (size_t k = s + 1; k-- > 0;) {
+    if (k != s) {
+      rem = shl(rem, 1);
+      if (a.bit(k)) {
+        if (rem.w.empty()) rem.w.push_back(0);
+        rem.w[0] |= 1u;
+      }
+    }
+    if (cmp(rem, m) >= 0) {
+      rem = sub(rem, m);
+      quo.w[k >> 5] |= 1u << (k & 31);
+    }
+  }
+  quo.trim();
+  if (q) *q = quo;
+  if (r) *r = rem;
+}
+
+inline BigU mod(const BigU& a, const BigU& m) {
+  BigU r;
+  divmod(a, m, nullptr, &r);
+  return r;
+}
+
+inline BigU mulmod(const BigU& a, const BigU& b, const BigU& m) { return mod(mul(a, b), m); }
+
+// (a - b) mod m for a, b < m
+inline BigU submod(const BigU& a, const BigU& b, const BigU& m) {
+  if (cmp(a, b) >= 0) return sub(a, b);
+  return sub(add(a, m), b);
+}
+
+// a^-1 mod m (extended Euclid); throws if not invertible (utils.py:71-76)
+inline BigU modinv(const BigU& a, const BigU& m) {
+  BigU r0 = m, r1 = mod(a, m), t0(0), t1(1);
+  while (!r1.is_zero()) {
+    BigU qq, rr;
+    divmod(r0, r1, &qq, &rr);
+    BigU t2 = submod(t0, mulmod(qq, t1, m), m);
+    r0 = r1;
+    r1 = rr;
+    t0 = t1;
+    t1 = t2;
+  }
+  if (!(r0.w.size() == 1 && r0.w[0] == 1)) throw std::runtime_error("modinv: no inverse exists");
+  return t0;
+}
+
+// a^e mod m, plain square-and-multiply (key setup only)
+inline BigU powmod(const BigU& a, const BigU& e, const BigU& m) {
+  BigU r = mod(BigU(1), m), b = mod(a, m);
+  for (size_t i = e.bits(); i-- > 0;) {
+    r = mulmod(r, r, m);
+    if (e.bit(i)) r = mulmod(r, b, m);
+  }
+  return r;
+}
+
+// -m^-1 mod 2^W for odd m (Newton iteration on the low word)
+inline uint32_t mont_ninv(uint32_t m0, int W) {
+  uint32_t x = 1;
+  for (int i = 0; i < 5; ++i) x *= 2u - m0 * x;  // x = m0^-1 mod 2^32
+  uint32_t r = (uint32_t)(0u - x);
+  return W == 32 ? r : (r & ((1u << W) - 1));
+}
+
+}  // namespace xhe

@@ -1,0 +1,534 @@
+// xhe: C-ABI over the gfx950 Paillier kernels (see include/xhe.h).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <cmath>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/xhe.h"
+#include "hostbn.hpp"
+#include "xhe_kernels.hpp"
+
+using namespace xhe;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t _e = (x);                                                                   \
+    if (_e != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// ------------------------------------------------------------------ shapes
+// Limb shapes per key size: MP2 for residues mod p^2/q^2, MP for mod p/q.
+struct Shape2048 {
+  using MP2 = Mont<74, 28, 1>;
+  using MP = Mont<37, 28, 1>;
+};
+struct Shape3072 {
+  using MP2 = Mont<110, 28, 2>;
+  using MP = Mont<56, 28, 2>;
+};
+
+struct ModSpec {
+  int S, W;
+  int S4() const { return (S + 3) & ~3; }
+};
+
+// ------------------------------------------------------------------ blob
+struct Blob {
+  std::vector<uint32_t> h;
+  size_t put(const std::vector<uint32_t>& v, size_t min_words = 0) {
+    size_t off = h.size();
+    size_t len = std::max(v.size(), min_words);
+    len = (len + 3) & ~(size_t)3;
+    h.resize(off + len, 0u);
+    std::copy(v.begin(), v.end(), h.begin() + off);
+    return off;
+  }
+  size_t put_limbs(const BigU& x, const ModSpec& s) { return put(x.to_limbs(s.W, s.S), s.S4()); }
+  size_t put_words(const BigU& x, int nw) {
+    std::vector<uint32_t> v(nw);
+    x.to_words(v.data(), nw);
+    return put(v);
+  }
+};
+
+struct ModOff {
+  size_t N, R1, R2, R3;
+  uint32_t n0inv;
+};
+
+ModOff put_mod(Blob& bl, const BigU& M, const ModSpec& s) {
+  ModOff o;
+  BigU R = pow2((size_t)s.W * s.S);
+  BigU R1 = mod(R, M);
+  BigU R2 = mulmod(R1, R1, M);
+  BigU R3 = mulmod(R2, R1, M);
+  o.N = bl.put_limbs(M, s);
+  o.R1 = bl.put_limbs(R1, s);
+  o.R2 = bl.put_limbs(R2, s);
+  o.R3 = bl.put_limbs(R3, s);
+  o.n0inv = mont_ninv(M.word(0), s.W);
+  return o;
+}
+
+}  // namespace
+
+struct xhe_key {
+  int device = 0;
+  int K = 0, nw = 0, n2w = 0;
+  bool priv = false, djn = false;
+  int rand_bits = 0, rand_words = 0;
+  ModSpec mp2{}, mp{};
+  uint32_t* d_blob = nullptr;
+  uint32_t* d_tab = nullptr;
+  KeyDev kd{};
+  std::vector<uint32_t> n_host;  // n words (for host-side checks)
+};
+
+namespace {
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    HIPCHK(hipGetDevice(&prev));
+    if (prev != dev) HIPCHK(hipSetDevice(dev));
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class Sh>
+void build_tables(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s) {
+  using MP2 = typename Sh::MP2;
+  uint32_t* d_ws = nullptr;
+  HIPCHK(hipMalloc(&d_ws, MP2::S4 * sizeof(uint32_t) * 4));
+  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, k->kd.win, k->kd.nwin, d_tab, d_ws);
+  HIPCHK(hipGetLastError());
+  int groups_per_block = 64 / MP2::TPI;
+  int blocks = (k->kd.nwin + groups_per_block - 1) / groups_per_block;
+  hipLaunchKernelGGL(k_tab_fill<MP2>, dim3(blocks), dim3(64), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(d_ws));
+}
+
+ModDev moddev(uint32_t* base, const ModOff& o) {
+  return ModDev{base + o.N, base + o.R1, base + o.R2, base + o.R3, o.n0inv};
+}
+
+void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, const BigU* h, int win) {
+  Blob bl;
+  const int K = k->K;
+  BigU n2 = mul(n, n);
+  size_t o_n = bl.put_words(n, k->nw);
+  size_t o_n2 = bl.put_words(n2, k->n2w);
+  BigU maxpos, minneg;
+  divmod(n, BigU(3), &maxpos, nullptr);
+  minneg = sub(n, maxpos);
+  size_t o_maxpos = bl.put_words(maxpos, k->nw);
+  size_t o_minneg = bl.put_words(minneg, k->nw);
+  // randomness bound (paillier.py:195 djn_exp_bound = 2^(bitlen(n)//2); :215 r < n)
+  k->rand_bits = k->djn ? (int)(n.bits() / 2) : (int)n.bits();
+  k->rand_words = (k->rand_bits + 31) / 32;
+
+  struct {
+    ModOff p2, q2, p, q;
+    size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
+    size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
+  } o;
+  int pm1_bits = 0, qm1_bits = 0;
+  if (k->priv) {
+    const BigU &P = *p, &Q = *q;
+    BigU p2 = mul(P, P), q2 = mul(Q, Q);
+    const ModSpec& s2 = k->mp2;
+    const ModSpec& s1 = k->mp;
+    o.p2 = put_mod(bl, p2, s2);
+    o.q2 = put_mod(bl, q2, s2);
+    BigU R2p = pow2((size_t)s2.W * s2.S);
+    BigU Rp2 = mod(R2p, p2), Rq2 = mod(R2p, q2);
+    // n R^2 mod P^2
+    o.nR2_p2 = bl.put_limbs(mulmod(mod(n, p2), mulmod(Rp2, Rp2, p2), p2), s2);
+    o.nR2_q2 = bl.put_limbs(mulmod(mod(n, q2), mulmod(Rq2, Rq2, q2), q2), s2);
+    // CRT constants (context.py:46)
+    BigU q2inv = modinv(q2, p2);
+    o.q2invR = bl.put_limbs(mulmod(q2inv, Rp2, p2), s2);
+    o.q2_lim = bl.put_limbs(q2, s2);
+    o.p2x4 = bl.put_limbs(shl(p2, 2), s2);
+    if (k->djn) {
+      o.hM_p2 = bl.put_limbs(mulmod(mod(*h, p2), Rp2, p2), s2);  // h_pow_n mod p^2 (context.py:63)
+      o.hM_q2 = bl.put_limbs(mulmod(mod(*h, q2), Rq2, q2), s2);
+    }
+    // mod p / q (decrypt)
+    o.p = put_mod(bl, P, s1);
+    o.q = put_mod(bl, Q, s1);
+    BigU pm1 = sub(P, BigU(1)), qm1 = sub(Q, BigU(1));
+    pm1_bits = (int)pm1.bits();
+    qm1_bits = (int)qm1.bits();
+    o.pm1 = bl.put_words(pm1, k->nw / 2 + 1);
+    o.qm1 = bl.put_words(qm1, k->nw / 2 + 1);
+    BigU T = pow2((size_t)s1.W * s1.S);
+    o.pinv = bl.put_limbs(modinv(P, T), s1);
+    o.qinv = bl.put_limbs(modinv(Q, T), s1);
+    // hp = L_p((n+1)^(p-1) mod p^2)^-1 mod p (context.py:47,193-194). By the
+    // binomial theorem (n+1)^(p-1) = 1 + (p-1) n (mod n^2, hence mod p^2).
+    auto hfun = [&](const BigU& X, const BigU& X2) {
+      BigU x = mod(add(BigU(1), mul(sub(X, BigU(1)), n)), X2);
+      BigU L;
+      divmod(sub(x, BigU(1)), X, &L, nullptr);
+      return modinv(L, X);
+    };
+    BigU hp = hfun(P, p2), hq = hfun(Q, q2);
+    BigU Rp = mod(T, P), Rq = mod(T, Q);
+    o.hpR = bl.put_limbs(mulmod(hp, Rp, P), s1);
+    o.hqR = bl.put_limbs(mulmod(hq, Rq, Q), s1);
+    o.qinvpR = bl.put_limbs(mulmod(modinv(Q, P), Rp, P), s1);  // context.py:43
+    o.q_lim = bl.put_limbs(Q, s1);
+    o.p2x = bl.put_limbs(shl(P, 1), s1);
+    o.p_lim = bl.put_limbs(P, s1);
+  }
+  // upload
+  HIPCHK(hipMalloc(&k->d_blob, bl.h.size() * sizeof(uint32_t)));
+  HIPCHK(hipMemcpy(k->d_blob, bl.h.data(), bl.h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  uint32_t* B = k->d_blob;
+  KeyDev& kd = k->kd;
+  kd.K = K;
+  kd.nw = k->nw;
+  kd.n2w = k->n2w;
+  kd.priv = k->priv;
+  kd.djn = k->djn;
+  kd.n_words = B + o_n;
+  kd.n2_words = B + o_n2;
+  kd.maxpos = B + o_maxpos;
+  kd.minneg = B + o_minneg;
+  if (k->priv) {
+    kd.p2 = moddev(B, o.p2);
+    kd.q2 = moddev(B, o.q2);
+    kd.nR2_p2 = B + o.nR2_p2;
+    kd.nR2_q2 = B + o.nR2_q2;
+    kd.q2invR_p2 = B + o.q2invR;
+    kd.q2_lim = B + o.q2_lim;
+    kd.p2x4_lim = B + o.p2x4;
+    kd.p = moddev(B, o.p);
+    kd.q = moddev(B, o.q);
+    kd.pm1_words = B + o.pm1;
+    kd.qm1_words = B + o.qm1;
+    kd.pm1_bits = pm1_bits;
+    kd.qm1_bits = qm1_bits;
+    kd.pinv_lim = B + o.pinv;
+    kd.qinv_lim = B + o.qinv;
+    kd.hpR = B + o.hpR;
+    kd.hqR = B + o.hqR;
+    kd.qinvpR = B + o.qinvpR;
+    kd.q_lim = B + o.q_lim;
+    kd.p2x_lim = B + o.p2x;
+    kd.p_lim = B + o.p_lim;
+    if (k->djn) {
+      kd.win = win;
+      kd.nwin = (k->rand_bits + win - 1) / win;
+      size_t rows = (size_t)kd.nwin << win;
+      size_t tab_words = rows * k->mp2.S4();
+      HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
+      kd.tab_p2 = k->d_tab;
+      kd.tab_q2 = k->d_tab + tab_words;
+      hipStream_t s;
+      HIPCHK(hipStreamCreate(&s));
+      if (K == 2048) {
+        build_tables<Shape2048>(k, kd.p2, B + o.hM_p2, k->d_tab, s);
+        build_tables<Shape2048>(k, kd.q2, B + o.hM_q2, k->d_tab + tab_words, s);
+      } else {
+        build_tables<Shape3072>(k, kd.p2, B + o.hM_p2, k->d_tab, s);
+        build_tables<Shape3072>(k, kd.q2, B + o.hM_q2, k->d_tab + tab_words, s);
+      }
+      HIPCHK(hipStreamDestroy(s));
+    }
+  }
+}
+
+int blocks_for(int64_t count, int tpi, int cap) {
+  int64_t threads = count * tpi;
+  int64_t b = (threads + 255) / 256;
+  if (b < 1) b = 1;
+  return (int)std::min<int64_t>(b, cap);
+}
+
+constexpr int64_t kChunk = 1 << 20;  // elements per launch chunk (bounds workspace)
+
+template <class Sh>
+void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct, hipStream_t s) {
+  using MP2 = typename Sh::MP2;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    int blocks = (int)((n * MP2::TPI + 255) / 256);
+    hipLaunchKernelGGL(k_djn_pow<MP2>, dim3(blocks, 2), dim3(256), 0, s, k->kd, m + (size_t)off * k->nw,
+                       r + (size_t)off * k->rand_words, k->rand_words, n, ws);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, n, ws, ct + (size_t)off * k->n2w);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
+
+template <class Sh>
+void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
+  using MP2 = typename Sh::MP2;
+  using MP = typename Sh::MP;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  int pow_blocks = (int)std::min<int64_t>((chunk * MP2::TPI + 255) / 256, 512);
+  int64_t groups = (int64_t)pow_blocks * 256 / MP2::TPI;
+  uint32_t *ws = nullptr, *xrows = nullptr, *mrows = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 17 * MP2::S4 * groups * sizeof(uint32_t), s));
+  HIPCHK(hipMallocAsync((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+  HIPCHK(hipMallocAsync((void**)&mrows, (size_t)2 * 2 * MP::S4 * chunk * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, ct + (size_t)off * k->n2w, n,
+                       xrows, ws);
+    HIPCHK(hipGetLastError());
+    int blocks = (int)((n * MP::TPI + 255) / 256);
+    hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, n, xrows, mrows);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_crt_dec<MP>, dim3(blocks), dim3(256), 0, s, k->kd, n, mrows, m + (size_t)off * k->nw);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+  HIPCHK(hipFreeAsync(xrows, s));
+  HIPCHK(hipFreeAsync(mrows, s));
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    return fail(XHE_EHIP, e.what());
+  } catch (const std::exception& e) {
+    return fail(XHE_EINVAL, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
+                   const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out) {
+  return guarded([&]() -> int {
+    if (!out || !n_words) return fail(XHE_EINVAL, "xhe_key_create: null argument");
+    *out = nullptr;
+    if (key_bits != 2048 && key_bits != 3072)
+      return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048 or 3072");
+    if ((p_words == nullptr) != (q_words == nullptr)) return fail(XHE_EINVAL, "xhe_key_create: need both p and q");
+    if (win_bits == 0) win_bits = 8;
+    if (win_bits != 4 && win_bits != 8) return fail(XHE_EINVAL, "xhe_key_create: win_bits must be 4 or 8");
+    std::unique_ptr<xhe_key> k(new xhe_key());
+    k->device = device;
+    k->K = key_bits;
+    k->nw = key_bits / 32;
+    k->n2w = 2 * k->nw;
+    k->priv = p_words != nullptr;
+    k->djn = h_pow_n_words != nullptr;
+    if (key_bits == 2048) {
+      k->mp2 = {Shape2048::MP2::S, Shape2048::MP2::W};
+      k->mp = {Shape2048::MP::S, Shape2048::MP::W};
+    } else {
+      k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
+      k->mp = {Shape3072::MP::S, Shape3072::MP::W};
+    }
+    BigU n = BigU::from_words(n_words, k->nw);
+    if ((int)n.bits() > key_bits || n.bits() + 2 < (size_t)key_bits)
+      return fail(XHE_EINVAL, "xhe_key_create: n does not match key_bits");
+    k->n_host.assign(n_words, n_words + k->nw);
+    BigU p, q, h;
+    if (k->priv) {
+      p = BigU::from_words(p_words, k->nw / 2);
+      q = BigU::from_words(q_words, k->nw / 2);
+      if (cmp(mul(p, q), n) != 0) return fail(XHE_EINVAL, "xhe_key_create: n != p*q");
+      if (p.bits() * 2 > (size_t)key_bits + 0 || q.bits() * 2 > (size_t)key_bits)
+        return fail(XHE_ENOTSUP, "xhe_key_create: p and q must each have key_bits/2 bits");
+      if ((p.w[0] & 1) == 0 || (q.w[0] & 1) == 0) return fail(XHE_EINVAL, "xhe_key_create: p, q must be odd");
+    }
+    if (k->djn) h = BigU::from_words(h_pow_n_words, k->n2w);
+    DevGuard dg(device);
+    key_create_impl(k.get(), n, k->priv ? &p : nullptr, k->priv ? &q : nullptr, k->djn ? &h : nullptr, win_bits);
+    *out = k.release();
+    return XHE_OK;
+  });
+}
+
+void xhe_key_destroy(xhe_key* key) {
+  if (!key) return;
+  int prev = -1;
+  if (hipGetDevice(&prev) == hipSuccess && prev != key->device) (void)hipSetDevice(key->device);
+  if (key->d_blob) (void)hipFree(key->d_blob);
+  if (key->d_tab) (void)hipFree(key->d_tab);
+  if (prev >= 0 && prev != key->device) (void)hipSetDevice(prev);
+  delete key;
+}
+
+int xhe_key_info(const xhe_key* key, int* key_bits, int* nw, int* n2w, int* rand_words, int* rand_bits, int* flags) {
+  if (!key) return fail(XHE_EINVAL, "xhe_key_info: null key");
+  if (key_bits) *key_bits = key->K;
+  if (nw) *nw = key->nw;
+  if (n2w) *n2w = key->n2w;
+  if (rand_words) *rand_words = key->rand_words;
+  if (rand_bits) *rand_bits = key->rand_bits;
+  if (flags) *flags = (key->priv ? 1 : 0) | (key->djn ? 2 : 0);
+  return XHE_OK;
+}
+
+int xhe_encode_f64(const xhe_key* key, const double* x_dev, int64_t count, int precision, int has_max,
+                   int max_exponent, uint32_t* m_dev, int32_t* exp_dev, int32_t* status_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!x_dev || !m_dev || !exp_dev || !status_dev)))
+      return fail(XHE_EINVAL, "xhe_encode_f64: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    int mode = precision < 0 ? 0 : 1;
+    // -ceil(log2(10) * precision) (encoder.py:39), computed exactly as Python does in float64
+    int e0 = precision < 0 ? 0 : -(int)std::ceil(std::log2(10.0) * (double)precision);
+    int blocks = (int)((count + 255) / 256);
+    hipLaunchKernelGGL(k_encode_f64, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x_dev, count, mode, e0,
+                       has_max, max_exponent, key->kd.n_words, key->nw, m_dev, exp_dev, status_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
+}
+
+int xhe_rand(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_t count, uint32_t* rand_dev,
+             int32_t* status_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || !seed32 || (count > 0 && !rand_dev)) return fail(XHE_EINVAL, "xhe_rand: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    ChaChaKey ck;
+    memcpy(ck.k, seed32, 32);
+    ck.nonce0 = (uint32_t)nonce;
+    ck.nonce1 = (uint32_t)(nonce >> 32);
+    int blocks = (int)((count + 255) / 256);
+    hipLaunchKernelGGL(k_rand_below, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ck, count, key->rand_words,
+                       key->rand_bits, key->djn ? (const uint32_t*)nullptr : key->kd.n_words, rand_dev, status_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
+}
+
+int xhe_encrypt(const xhe_key* key, const uint32_t* m_dev, const uint32_t* rand_dev, int64_t count, uint32_t* ct_dev,
+                void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!m_dev || !ct_dev))) return fail(XHE_EINVAL, "xhe_encrypt: null argument");
+    if (count <= 0) return XHE_OK;
+    if (!(key->priv && key->djn && rand_dev))
+      return fail(XHE_ENOTSUP, "xhe_encrypt: only DJN private-key obfuscated encryption is built");
+    DevGuard dg(key->device);
+    if (key->K == 2048) encrypt_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, (hipStream_t)stream);
+    else encrypt_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
+int xhe_decrypt(const xhe_key* key, const uint32_t* ct_dev, int64_t count, uint32_t* m_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!ct_dev || !m_dev))) return fail(XHE_EINVAL, "xhe_decrypt: null argument");
+    if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    if (key->K == 2048) decrypt_impl<Shape2048>(key, ct_dev, count, m_dev, (hipStream_t)stream);
+    else decrypt_impl<Shape3072>(key, ct_dev, count, m_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
+int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev, int64_t count, double* f64_dev,
+               float* f32_dev, int32_t* status_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!m_dev || !exp_dev || !f64_dev || !f32_dev || !status_dev)))
+      return fail(XHE_EINVAL, "xhe_decode: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    int blocks = (int)((count + 255) / 256);
+    hipLaunchKernelGGL(k_decode, dim3(blocks), dim3(256), 0, (hipStream_t)stream, m_dev, exp_dev, count, key->kd,
+                       f64_dev, f32_dev, status_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
+}
+
+static int host_roundtrip(const xhe_key* key, const uint32_t* in, size_t in_words, uint32_t* outp, size_t out_words,
+                          const uint32_t* in2, size_t in2_words, bool enc) {
+  DevGuard dg(key->device);
+  hipStream_t s;
+  HIPCHK(hipStreamCreate(&s));
+  uint32_t *d_in = nullptr, *d_in2 = nullptr, *d_out = nullptr;
+  HIPCHK(hipMalloc(&d_in, std::max<size_t>(in_words, 1) * 4));
+  HIPCHK(hipMalloc(&d_out, std::max<size_t>(out_words, 1) * 4));
+  if (in2) HIPCHK(hipMalloc(&d_in2, std::max<size_t>(in2_words, 1) * 4));
+  HIPCHK(hipMemcpyAsync(d_in, in, in_words * 4, hipMemcpyHostToDevice, s));
+  if (in2) HIPCHK(hipMemcpyAsync(d_in2, in2, in2_words * 4, hipMemcpyHostToDevice, s));
+  int rc;
+  int64_t count = enc ? (int64_t)(in_words / key->nw) : (int64_t)(in_words / key->n2w);
+  if (enc) rc = xhe_encrypt(key, d_in, d_in2, count, d_out, s);
+  else rc = xhe_decrypt(key, d_in, count, d_out, s);
+  if (rc == XHE_OK) HIPCHK(hipMemcpyAsync(outp, d_out, out_words * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  if (d_in2) (void)hipFree(d_in2);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!m || !ct))) return fail(XHE_EINVAL, "xhe_encrypt_host: null argument");
+    if (count <= 0) return XHE_OK;
+    return host_roundtrip(key, m, (size_t)count * key->nw, ct, (size_t)count * key->n2w, rand,
+                          rand ? (size_t)count * key->rand_words : 0, true);
+  });
+}
+
+int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint32_t* m) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!ct || !m))) return fail(XHE_EINVAL, "xhe_decrypt_host: null argument");
+    if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
+    if (count <= 0) return XHE_OK;
+    return host_roundtrip(key, ct, (size_t)count * key->n2w, m, (size_t)count * key->nw, nullptr, 0, false);
+  });
+}
+
+int xhe_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int xhe_synchronize(void* stream) {
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return fail(XHE_EHIP, hipGetErrorString(e));
+  return XHE_OK;
+}
+
+const char* xhe_last_error(void) { return g_err.c_str(); }
+const char* xhe_version(void) { return "xhe 0.1 gfx950"; }
+
+}  // extern "C"

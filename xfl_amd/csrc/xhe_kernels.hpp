@@ -1,0 +1,571 @@
+// Paillier hot-path kernels (gfx950). One residue per TPI-lane group; see
+// bn_dev.hpp for the Montgomery representation.
+//
+// Reference semantics (paths under /root/reference/python):
+//   encode            common/crypto/paillier/encoder.py:29-54, paillier.py:279-282
+//   raw encrypt       paillier.py:283            c0 = (1 + n*m) mod n^2
+//   DJN obfuscation   paillier.py:193-209        c0 * h^a mod n^2 (CRT over p^2, q^2)
+//   decrypt           paillier.py:341-368        L(c^(p-1) mod p^2) * hp mod p, CRT
+//   decode            encoder.py:56-64, paillier.py:396-403
+#pragma once
+#include "bn_dev.hpp"
+
+namespace xhe {
+
+struct ModDev {
+  const uint32_t* N;   // S W-limbs (row of S4 words)
+  const uint32_t* R1;  // R mod N
+  const uint32_t* R2;  // R^2 mod N
+  const uint32_t* R3;  // R^3 mod N
+  uint32_t n0inv;
+};
+
+// All pointers are device pointers into the key blob. Limb rows are padded to
+// a multiple of 4 words and 16-byte aligned.
+struct KeyDev {
+  int K, nw, n2w;  // key bits, 32-bit words of n and of n^2
+  int priv, djn;
+  const uint32_t* n_words;   // n (nw words)
+  const uint32_t* n2_words;  // n^2 (n2w words)
+  const uint32_t* maxpos;    // n // 3 (nw words)
+  const uint32_t* minneg;    // n - n // 3 (nw words)
+  // ---- mod p^2 / q^2 (shape MP2)
+  ModDev p2, q2;
+  const uint32_t* nR2_p2;     // n * R^2 mod p^2
+  const uint32_t* nR2_q2;     // n * R^2 mod q^2
+  const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
+  const uint32_t* q2_lim;     // q^2 (MP2 limbs)
+  const uint32_t* p2x4_lim;   // 4 p^2 (MP2 limbs)
+  const uint32_t* tab_p2;     // [nwin][2^win][S4] h^(d*2^(win*w)) * R mod p^2
+  const uint32_t* tab_q2;
+  int win, nwin;
+  // ---- mod p / q (shape MP), decrypt
+  ModDev p, q;
+  const uint32_t* pm1_words;  // p - 1 (nw/2 words)
+  const uint32_t* qm1_words;
+  int pm1_bits, qm1_bits;
+  const uint32_t* pinv_lim;   // p^-1 mod 2^(W*S) (MP limbs)
+  const uint32_t* qinv_lim;
+  const uint32_t* hpR;        // hp * R mod p
+  const uint32_t* hqR;
+  const uint32_t* qinvpR;     // (q^-1 mod p) * R mod p
+  const uint32_t* q_lim;      // q (MP limbs)
+  const uint32_t* p2x_lim;    // 2 p (MP limbs)
+  const uint32_t* p_lim;      // p (MP limbs)
+};
+
+// ============================================================== encode
+// status codes per element (mirrors the exceptions the reference raises)
+enum : int32_t { ST_OK = 0, ST_OVERFLOW = 1, ST_VALUE = 2 };
+
+// One element per thread: float64 x -> m = round_half_even(x * 2^-e) mod n,
+// e from `mode` (0: frexp(x)-53, i.e. precision None; 1: fixed e0) clamped by
+// max_exponent when has_max. Writes nw words of m and the exponent.
+__global__ void k_encode_f64(const double* __restrict__ x, int64_t count, int mode, int e0, int has_max,
+                             int max_exp, const uint32_t* __restrict__ n_words, int nw,
+                             uint32_t* __restrict__ m_out, int32_t* __restrict__ e_out,
+                             int32_t* __restrict__ status) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  double v = x[i];
+  uint64_t bits = __double_as_longlong(v);
+  int neg = (int)(bits >> 63);
+  int bexp = (int)((bits >> 52) & 0x7FF);
+  uint64_t frac = bits & ((1ull << 52) - 1);
+  int e;
+  if (mode == 0) {
+    // math.frexp(x)[1] - 53; frexp(0) = (0, 0); frexp(inf/nan) = (x, 0)
+    int fe;
+    if (bexp == 0x7FF || (bexp == 0 && frac == 0)) fe = 0;
+    else if (bexp == 0) fe = -1022 - (__clzll(frac) - 12) ;  // subnormal: frexp exponent
+    else fe = bexp - 1022;
+    e = fe - 53;
+  } else {
+    e = e0;
+  }
+  if (has_max && max_exp < e) e = max_exp;
+  uint32_t* mo = m_out + (size_t)i * nw;
+  e_out[i] = e;
+  int32_t st = ST_OK;
+  // x * (1 << -e): negative shift -> ValueError; shift >= 1024 -> int->float OverflowError
+  if (-e < 0) st = ST_VALUE;
+  else if (-e >= 1024) st = ST_OVERFLOW;
+  else if (bexp == 0x7FF) st = frac ? ST_VALUE : ST_OVERFLOW;  // round(nan) / round(inf)
+  // M * 2^E exact decomposition
+  uint64_t M;
+  int E;
+  if (bexp == 0) { M = frac; E = -1074; } else { M = frac | (1ull << 52); E = bexp - 1075; }
+  int sh = E - e;  // y = M * 2^sh
+  // float product overflow (|y| >= 2^1024) -> inf -> round(inf) OverflowError
+  if (st == ST_OK && M != 0) {
+    int top = 64 - __clzll(M) + sh;  // y < 2^top
+    if (top > 1024) st = ST_OVERFLOW;
+  }
+  for (int k = 0; k < nw; ++k) mo[k] = 0;
+  status[i] = st;
+  if (st != ST_OK || M == 0) return;
+  // integer q = round_half_even(M * 2^sh)
+  if (sh >= 0) {
+    int w = sh >> 5, b = sh & 31;
+    uint64_t lo = M << b;                                 // bits [w*32, w*32+64)
+    uint32_t hi = b ? (uint32_t)(M >> (64 - b)) : 0u;     // bits [w*32+64, +96)
+    if (w < nw) mo[w] = (uint32_t)lo;
+    if (w + 1 < nw) mo[w + 1] = (uint32_t)(lo >> 32);
+    if (w + 2 < nw) mo[w + 2] = hi;
+  } else {
+    int r = -sh;
+    uint64_t q, rem, half;
+    if (r >= 64) { q = 0; rem = M; half = (r == 64) ? (1ull << 63) : ~0ull; if (r > 64) { q = 0; rem = 0; } }
+    else { q = M >> r; rem = M & ((1ull << r) - 1); half = 1ull << (r - 1); }
+    if (r <= 64 && (rem > half || (rem == half && (q & 1)))) q += 1;
+    mo[0] = (uint32_t)q;
+    mo[1] = (uint32_t)(q >> 32);
+  }
+  if (neg) {
+    // m = n - |y| (|y| < 2^1077 < n for K >= 2048), or 0 when y == 0
+    bool zero = true;
+    for (int k = 0; k < nw; ++k) zero &= mo[k] == 0;
+    if (!zero) {
+      int64_t br = 0;
+      for (int k = 0; k < nw; ++k) {
+        int64_t d = (int64_t)n_words[k] - (int64_t)mo[k] - br;
+        br = d < 0;
+        mo[k] = (uint32_t)(d + (br << 32));
+      }
+    }
+  }
+}
+
+// ============================================================== ChaCha20
+XHE_DEV uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define XHE_QR(a, b, c, d) \
+  a += b; d ^= a; d = rotl32(d, 16); c += d; b ^= c; b = rotl32(b, 12); \
+  a += b; d ^= a; d = rotl32(d, 8);  c += d; b ^= c; b = rotl32(b, 7);
+
+XHE_DEV void chacha20_block(const uint32_t key[8], uint32_t nonce0, uint32_t nonce1, uint64_t ctr, uint32_t out[16]) {
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                    (uint32_t)ctr, (uint32_t)(ctr >> 32), nonce0, nonce1};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = s[i];
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    XHE_QR(x[0], x[4], x[8], x[12]) XHE_QR(x[1], x[5], x[9], x[13])
+    XHE_QR(x[2], x[6], x[10], x[14]) XHE_QR(x[3], x[7], x[11], x[15])
+    XHE_QR(x[0], x[5], x[10], x[15]) XHE_QR(x[1], x[6], x[11], x[12])
+    XHE_QR(x[2], x[7], x[8], x[13]) XHE_QR(x[3], x[4], x[9], x[14])
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+
+struct ChaChaKey { uint32_t k[8]; uint32_t nonce0, nonce1; };
+
+// Uniform integers in [1, 2^bits) (DJN a, paillier.py:195) when bound == null,
+// else in [1, bound) by rejection (non-DJN r in [1, n), paillier.py:215).
+// `words` 32-bit words per element; element i uses counter block
+// (i * 16 + attempt) * blocks_per_draw.
+__global__ void k_rand_below(ChaChaKey ck, int64_t count, int words, int bits, const uint32_t* __restrict__ bound,
+                             uint32_t* __restrict__ out, int32_t* __restrict__ status) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t* o = out + (size_t)i * words;
+  const int blocks = (words + 15) / 16;
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    for (int b = 0; b < blocks; ++b) {
+      uint32_t ks[16];
+      chacha20_block(ck.k, ck.nonce0, ck.nonce1, ((uint64_t)i * 64 + attempt) * blocks + b, ks);
+      for (int t = 0; t < 16 && b * 16 + t < words; ++t) o[b * 16 + t] = ks[t];
+    }
+    // mask to `bits`
+    for (int k = 0; k < words; ++k) {
+      int lo = 32 * k;
+      if (lo >= bits) o[k] = 0;
+      else if (bits - lo < 32) o[k] &= (1u << (bits - lo)) - 1u;
+    }
+    bool zero = true;
+    for (int k = 0; k < words; ++k) zero &= o[k] == 0;
+    bool ok = !zero;
+    if (ok && bound) {  // o < bound ?
+      int c = 0;
+      for (int k = words - 1; k >= 0 && c == 0; --k) c = o[k] < bound[k] ? -1 : (o[k] > bound[k] ? 1 : 0);
+      ok = c < 0;
+    }
+    if (ok) { if (status) status[i] = ST_OK; return; }
+  }
+  if (status) status[i] = ST_VALUE;
+}
+
+// ============================================================== encrypt
+template <class MP2>
+XHE_DEV void fixed_base_pow(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* tab, int win, int nwin,
+                            const uint32_t* __restrict__ a_words) {
+  const int rows = 1 << win;
+  for (int w = 0; w < nwin; ++w) {
+    int bit = w * win;
+    uint32_t d = (a_words[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encryption, DJN private key (CRT over p^2, q^2)   (paillier.py:193-209, 283)
+//   c_P = (1 + n m) * h_P^a mod P^2        k_djn_pow, grid.y = prime (0: p, 1: q)
+//   c   = c_q + q^2 ((c_p + 4p^2 - c_q) (q^2)^-1 mod p^2)    k_crt_enc
+// Element rows live in ws as [prime][2*S4 limbs][count] (limb i of element e
+// at row[i * count + e]); the second half of each row is wide-product scratch.
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* __restrict__ m_words,
+                                                    const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                    uint32_t* __restrict__ ws) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (e >= count) return;
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
+  MP2 M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{prime ? key.nR2_q2 : key.nR2_p2});  // n m R mod P^2
+  M.add_row(b, md.R1);                              // (1 + n m) R
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  const int rows = 1 << key.win;
+  for (int w = 0; w < key.nwin; ++w) {
+    int bit = w * key.win;
+    uint32_t d = (ae[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
+  }
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, int64_t count, uint32_t* __restrict__ ws,
+                                                    uint32_t* __restrict__ out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (e >= count) return;
+  uint32_t* rp = ws + e;
+  uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + e;
+  const int st = (int)count;
+  MP2 M;
+  M.init(key.p2.N, key.p2.n0inv);
+  uint32_t b[MP2::L];
+  M.load_strided(b, rp, st);
+  M.add_sub_rows(b, key.p2x4_lim, rq, st);
+  M.mul(b, ARow{key.q2invR_p2});
+  M.reduce_once(b);
+  M.wide_mul_add_store(b, ARow{key.q2_lim}, rq, st, out + (size_t)e * key.n2w, key.n2w);
+}
+
+// ---------------------------------------------------------------------------
+// Decryption (paillier.py:341-368)
+// k_dec_pow: X_P = (c^(P-1) mod P^2) - 1 for one prime (grid.y), written to
+// xrows [prime][S4][count]. Per-group 4-bit window tables live in wsg
+// (17 interleaved rows per group, grid-stride loop over elements).
+template <class MP2>
+XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* ex, int ebits,
+                             uint32_t* tab, uint32_t* sq, int st) {
+  const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
+  M.store_strided(b, tab + rs, st);         // tab[1] = b
+  wave_sync_mem_();
+  for (int t = 2; t < 16; ++t) {
+    M.mul(b, AStrided{tab + rs, st});  // tab[t] = tab[t-1] * tab[1]
+    M.store_strided(b, tab + rs * t, st);
+  }
+  wave_sync_mem_();
+  int nwin = (ebits + 3) / 4;
+  int top = nwin - 1;
+  uint32_t d = (ex[(top * 4) >> 5] >> ((top * 4) & 31)) & 15u;
+  M.load_strided(b, tab + rs * d, st);  // top window is nonzero
+  for (int w = top - 1; w >= 0; --w) {
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      M.store_strided(b, sq, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq, st});
+    }
+    uint32_t dw = (ex[(w * 4) >> 5] >> ((w * 4) & 31)) & 15u;
+    if (dw) M.mul(b, AStrided{tab + rs * dw, st});
+  }
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* __restrict__ c_words, int64_t count,
+                                                    uint32_t* __restrict__ xrows, uint32_t* __restrict__ ws) {
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
+  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
+  const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MP2::TPI;
+  const int64_t gid0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  const int st = (int)G_total;
+  const size_t rs = (size_t)MP2::S4 * st;
+  uint32_t* tab = ws + (size_t)prime * 17 * rs + gid0;  // rows 0..15
+  uint32_t* sq = tab + 16 * rs;
+  const int n2w = key.n2w;
+  for (int64_t e = gid0; e < count; e += G_total) {
+    const uint32_t* cw = c_words + (size_t)e * n2w;
+    MP2 M;
+    M.init(md.N, md.n0inv);
+    uint32_t b[MP2::L];
+    // high limbs [S, 2S) of c into the sq row, then REDC(c) * R^3 = c R mod P^2
+    {
+      const int g = MP2::G::g();
+#pragma unroll
+      for (int j = 0; j < MP2::L; ++j) {
+        int J = MP2::S + g * MP2::L + j;
+        int bit = MP2::W * J, k = bit >> 5, sh = bit & 31;
+        uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+        sq[(size_t)(g * MP2::L + j) * st] = (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2::MASK;
+      }
+      if (g == 0)
+        for (int j = MP2::S; j < MP2::S4; ++j) sq[(size_t)j * st] = 0u;
+    }
+    M.load_words(b, cw, n2w);  // low S limbs
+    wave_sync_mem_();
+    M.redc_wide(b, AStrided{sq, st});
+    M.mul(b, ARow{md.R3});
+    pow_uniform_exp(M, b, ex, ebits, tab, sq, st);
+    M.mul(b, AOne{});
+    M.reduce_once(b);  // x = c^(P-1) mod P^2, x = 1 (mod P)
+    // X = x - 1 = x + (2^(W S) - 1) - 2^(W S): add all-ones, drop the top carry
+    uint64_t T[MP2::L];
+#pragma unroll
+    for (int j = 0; j < MP2::L; ++j) T[j] = (uint64_t)b[j] + (uint64_t)MP2::MASK;
+    M.normalize(T, b);
+    M.store_strided(b, xrows + (size_t)prime * MP2::S4 * count + e, (int)count);
+  }
+}
+
+// k_dec_fin: m_P = (X_P * P^-1 mod 2^(W*S1)) * hP mod P  (exact division: L_P,
+// context.py:190-194), written to mrows [prime][2*S4][count] (MP limbs).
+template <class MP2, class MP>
+__global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, int64_t count, const uint32_t* __restrict__ xrows,
+                                                    uint32_t* __restrict__ mrows) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP::TPI;
+  if (e >= count) return;
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q : key.p;
+  const uint32_t* Pinv = prime ? key.qinv_lim : key.pinv_lim;
+  const int st = (int)count;
+  uint32_t* mrow = mrows + (size_t)prime * 2 * MP::S4 * count + e;
+  MP M;
+  M.init(md.N, md.n0inv);
+  uint32_t q[MP::L];
+  M.load_strided(q, xrows + (size_t)prime * MP2::S4 * count + e, st);  // low S1 limbs of X
+  {
+    const int g = MP::G::g();
+    const bool lead = g == 0;
+    uint64_t T[MP::L];
+#pragma unroll
+    for (int j = 0; j < MP::L; ++j) T[j] = 0;
+    for (int i0 = 0; i0 < MP::S4; i0 += 4) {
+      uint4 a4 = ARow{Pinv}.load4(i0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (i0 + r < MP::S) {
+          uint32_t ai = comp4(a4, r);
+          uint64_t x0 = mad64(ai, q[0], T[0]);
+          if (lead) mrow[(size_t)(i0 + r) * st] = (uint32_t)x0 & MP::MASK;
+#pragma unroll
+          for (int j = 1; j < MP::L; ++j) T[j - 1] = mad64(ai, q[j], T[j]);
+          T[MP::L - 1] = MP::G::from_next64(x0);
+          T[0] += lead ? (x0 >> MP::W) : 0ull;
+        }
+      }
+    }
+  }
+  wave_sync_mem_();
+  M.load_strided(q, mrow, st);  // L_P(x)
+  M.mul(q, ARow{prime ? key.hqR : key.hpR});
+  M.reduce_once(q);
+  M.store_strided(q, mrow, st);
+}
+
+// k_crt_dec: u = (mp + 2p - mq) q^-1 mod p ; m = mq + u q   (utils.py:38-43)
+template <class MP>
+__global__ void __launch_bounds__(256, 2) k_crt_dec(KeyDev key, int64_t count, uint32_t* __restrict__ mrows,
+                                                    uint32_t* __restrict__ m_out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP::TPI;
+  if (e >= count) return;
+  const int st = (int)count;
+  uint32_t* rp = mrows + e;
+  uint32_t* rq = mrows + (size_t)2 * MP::S4 * count + e;
+  MP M;
+  M.init(key.p.N, key.p.n0inv);
+  uint32_t u[MP::L];
+  M.load_strided(u, rp, st);
+  M.add_sub_rows(u, key.p2x_lim, rq, st);
+  M.mul(u, ARow{key.qinvpR});
+  M.reduce_once(u);
+  M.wide_mul_add_store(u, ARow{key.q_lim}, rq, st, m_out + (size_t)e * key.nw, key.nw);
+}
+
+// ============================================================== tables
+// Fixed-base table for h (Montgomery form row `hM`, canonical):
+//   tab[w][d] = h^(d * 2^(win*w)) * R mod M, d in [0, 2^win)
+// k_tab_bases: one group walks the squaring chain, writing tab[w][1].
+template <class MP2>
+__global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* hM, int win, int nwin, uint32_t* tab, uint32_t* ws) {
+  if (blockIdx.x != 0 || threadIdx.x >= MP2::TPI) return;
+  MP2 M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_row(b, hM);
+  const int rows = 1 << win;
+  for (int w = 0; w < nwin; ++w) {
+    M.store_row(b, tab + ((size_t)w * rows + 1) * MP2::S4);
+    if (w + 1 == nwin) break;
+    for (int s = 0; s < win; ++s) {
+      M.store_row(b, ws);
+      wave_sync_mem_();
+      M.mul(b, ARow{ws});
+      M.reduce_once(b);
+    }
+  }
+}
+
+// k_tab_fill: one group per window w: tab[w][0] = R, tab[w][d] = tab[w][d-1] * tab[w][1]
+template <class MP2>
+__global__ void __launch_bounds__(64, 2) k_tab_fill(ModDev md, int win, int nwin, uint32_t* tab) {
+  const int w = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI);
+  if (w >= nwin) return;
+  MP2 M;
+  M.init(md.N, md.n0inv);
+  const int rows = 1 << win;
+  uint32_t* t = tab + (size_t)w * rows * MP2::S4;
+  uint32_t b[MP2::L];
+  M.load_row(b, md.R1);
+  M.reduce_once(b);
+  M.store_row(b, t);
+  M.load_row(b, t + MP2::S4);
+  for (int d = 2; d < rows; ++d) {
+    M.mul(b, ARow{t + MP2::S4});
+    M.reduce_once(b);
+    M.store_row(b, t + (size_t)d * MP2::S4);
+  }
+}
+
+// Montgomery product of two rows (host-side setup helper / unit tests):
+// out = x * y * R^-1 mod M, canonical.
+template <class MP2>
+__global__ void k_mont_rows(ModDev md, const uint32_t* x, const uint32_t* y, uint32_t* out, int64_t count) {
+  int64_t gidx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (gidx >= count) return;
+  MP2 M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_row(b, x + (size_t)gidx * MP2::S4);
+  M.mul(b, ARow{y + (size_t)gidx * MP2::S4});
+  M.reduce_once(b);
+  M.store_row(b, out + (size_t)gidx * MP2::S4);
+}
+
+// ============================================================== decode
+// m (nw words) and exponent -> float64 as Paillier.decrypt would hand it to
+// astype(np.float32): e < 0: RNE53(v * 2^e) with 2^e a double (0 below
+// 2^-1074), subnormals rounded again, overflow to inf (encoder.py:63);
+// e >= 0: float(mpz(v << e)) truncated toward zero (gmpy2 2.0.8, measured).
+// status: 0 ok, 1 decode OverflowError (max_pos < m < min_neg), 3 mpz too
+// large for float (astype OverflowError).
+__global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __restrict__ exps, int64_t count,
+                         KeyDev key, double* __restrict__ out_f64, float* __restrict__ out_f32,
+                         int32_t* __restrict__ status) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int nw = key.nw;
+  const uint32_t* m = m_words + (size_t)i * nw;
+  int e = exps[i];
+  // compare with min_neg / max_pos
+  auto cmpw = [&](const uint32_t* a, const uint32_t* b) {
+    for (int k = nw - 1; k >= 0; --k) if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return 0;
+  };
+  int neg = cmpw(m, key.minneg) >= 0;
+  int32_t st = 0;
+  if (!neg && cmpw(m, key.maxpos) > 0) st = 1;
+  // magnitude: top 128 bits window of |v|
+  // find bit length
+  int bl = 0;
+  // |v| = neg ? n - m : m ; compute words on the fly from the top
+  // (borrow needs low words, so compute full magnitude into a small cache)
+  // nw <= 96 for K <= 3072
+  uint32_t mag[96];
+  int64_t br = 0;
+  for (int k = 0; k < nw; ++k) {
+    int64_t d = neg ? ((int64_t)key.n_words[k] - (int64_t)m[k] - br) : (int64_t)m[k];
+    if (neg) { br = d < 0; d += br << 32; }
+    mag[k] = (uint32_t)d;
+  }
+  for (int k = nw - 1; k >= 0; --k) if (mag[k]) { bl = 32 * k + 32 - __clz(mag[k]); break; }
+  double res;
+  if (st != 0) { res = 0.0; }
+  else if (bl == 0) {
+    res = 0.0;
+    if (e < -1074 && neg) res = -0.0;  // never: v == 0 is not negative
+  } else {
+    // q = RNE53(|v|) as (mant, shift): |v| ~ mant * 2^shift
+    uint64_t mant;
+    int shift;
+    if (bl <= 53) {
+      mant = (uint64_t)mag[0] | ((uint64_t)(nw > 1 ? mag[1] : 0) << 32);
+      shift = 0;
+    } else {
+      int s = bl - 53;
+      // extract 53 bits starting at bit s, plus round/sticky
+      auto bitsat = [&](int pos) -> uint64_t {  // 64 bits starting at pos
+        int k = pos >> 5, o = pos & 31;
+        uint64_t w0 = k < nw ? mag[k] : 0, w1 = k + 1 < nw ? mag[k + 1] : 0, w2 = k + 2 < nw ? mag[k + 2] : 0;
+        uint64_t lo = (w0 | (w1 << 32)) >> o;
+        if (o) lo |= w2 << (64 - o);
+        return lo;
+      };
+      mant = bitsat(s) & ((1ull << 53) - 1);
+      uint64_t rbit = (bitsat(s - 1) & 1ull);
+      bool sticky = false;
+      for (int k = 0; k < ((s - 1) >> 5); ++k) sticky |= mag[k] != 0;
+      int sb = (s - 1) & 31;
+      if (sb) sticky |= (mag[(s - 1) >> 5] & ((1u << sb) - 1u)) != 0;
+      shift = s;
+      if (e >= 0) {
+        // gmpy2 mpz->float truncates: keep mant, no rounding
+      } else if (rbit && (sticky || (mant & 1))) {
+        mant += 1;
+        if (mant >> 53) { mant >>= 1; shift += 1; }
+      }
+    }
+    if (e >= 0) {
+      int top = bl + e;
+      if (top > 1024) { st = 3; res = 0.0; }
+      else res = ldexp((double)mant, shift + e);
+    } else if (e < -1074) {
+      res = 0.0;
+    } else {
+      int ex2 = shift + e;
+      int mb = 64 - __clzll(mant);
+      int top = mb + ex2;
+      if (top > 1024) res = __longlong_as_double(0x7FF0000000000000ll);
+      else if (top <= -1021) {
+        int sh2 = -1074 - ex2;  // bits to drop for the subnormal grid
+        if (sh2 <= 0) res = ldexp((double)mant, ex2);
+        else if (sh2 >= 64) res = 0.0;
+        else {
+          uint64_t qv = mant >> sh2, rem = mant & ((1ull << sh2) - 1), half = 1ull << (sh2 - 1);
+          if (rem > half || (rem == half && (qv & 1))) qv += 1;
+          res = ldexp((double)qv, -1074);
+        }
+      } else res = ldexp((double)mant, ex2);
+    }
+    if (neg) res = -res;
+  }
+  if (bl == 0 && e < -1074) res = 0.0;
+  if (neg && e < -1074 && st == 0) res = -0.0;
+  out_f64[i] = res;
+  out_f32[i] = (float)res;
+  status[i] = st;
+}
+
+}  // namespace xhe
