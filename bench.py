@@ -1,0 +1,196 @@
+"""Throughput benchmark: 2048-bit Paillier encryptions/s, device-resident.
+
+One step = the label-trainer encryption of one synthetic batch
+(logistic_regression/label_trainer.py:193-197 at BASELINE config 2 size):
+    encode float64 -> m (precision 7)   (encoder.py:29-54)
+    draw DJN obfuscation exponents a   (paillier.py:195, device ChaCha20)
+    c = (1 + n m) h^a mod n^2 via CRT  (paillier.py:189-209, 283)
+for N elements per GPU that are already resident in HBM. With --gpus > 1 each
+rank encrypts its own shard (weak scaling) and the step ends with an RCCL
+all-gather of the ciphertext shards over xGMI, so every rank holds the whole
+vector (the reassembly step of SURVEY.md 8(e)).
+
+    python bench.py [--gpus N --steps K --warmup W --n ELEMENTS]
+"""
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+PEAK_MAC_PER_S = 1024 * 16 * 2.4e9  # v_mad_u64_u32: 4 cycles/wave64 on 1024 SIMDs at 2.4 GHz (tools/microbench)
+
+
+def make_key(bits, seed):
+    """Deterministic DJN key (context.py:73-84 / :123-150 with a seeded RNG)."""
+    from xfl_amd.paillier.utils import getprimeover
+    rng = random.Random(seed)
+    while True:
+        p = getprimeover(bits // 2, rng=rng)
+        q = getprimeover(bits // 2, rng=rng)
+        if p != q and math.gcd(p - 1, q - 1) == 2:
+            break
+    n = p * q
+    x = rng.getrandbits(n.bit_length()) | (1 << (n.bit_length() - 1))
+    h_pow_n = pow(-(x * x), n, n * n)
+    return p, q, n, h_pow_n
+
+
+def algorithmic_macs_per_element(bits, win, rand_bits):
+    """32-bit-limb MACs of the fixed-base DJN-CRT encryption (SURVEY 8(d) model):
+    per prime 1 (n m R) + nwin table products + 1 (from Montgomery) CIOS
+    products of s = bits/32 limbs at 2s^2+s MACs each; plus the CRT product and
+    the q^2 * h wide multiply (s^2)."""
+    s = bits // 32
+    nwin = -(-rand_bits // win)
+    prod = 2 * s * s + s
+    return 2 * (nwin + 2) * prod + prod + s * s, 2 * nwin * prod
+
+
+def cpu_baseline(bits, seconds, cores):
+    """Reference-algorithm port (oracle/paillier_oracle.py, pure-Python pow,
+    the GMP-free restatement) timed on this host for a bounded sample."""
+    import multiprocessing as mp
+    from oracle import bench_cpu
+    with mp.get_context("fork").Pool(cores) as pool:
+        t0 = time.time()
+        counts = pool.map(bench_cpu.encrypt_for, [(bits, seconds, i) for i in range(cores)])
+        wall = time.time() - t0
+    total = sum(counts)
+    return {"value": total / wall, "unit": "encrypts/s", "cores": cores, "kind": "port",
+            "sample": f"{total} DJN-CRT private-key encryptions of float64 plaintexts (precision 7), "
+                      f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
+    ap.add_argument("--key-bits", type=int, default=2048)
+    ap.add_argument("--win", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from xfl_amd import _native as nat
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    bits = args.key_bits
+    p, q, n, h = make_key(bits, seed=2024)
+    t_key = time.time()
+    dk = nat.DeviceKey(bits, n, p, q, h, device=local, win_bits=args.win)
+    torch.cuda.synchronize()
+    t_key = time.time() - t_key
+    L = nat.lib()
+
+    N = args.n
+    rng = np.random.default_rng(0 + rank)
+    x = torch.from_numpy(rng.standard_normal(N)).to("cuda")
+    m = torch.empty((N, dk.nw), dtype=torch.int32, device="cuda")
+    ex = torch.empty(N, dtype=torch.int32, device="cuda")
+    st = torch.empty(N, dtype=torch.int32, device="cuda")
+    rnd = torch.empty((N, dk.rand_words), dtype=torch.int32, device="cuda")
+    ct = torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda")
+    gathered = torch.empty((world * N, dk.n2w), dtype=torch.int32, device="cuda") if world > 1 else None
+    seed32 = os.urandom(32)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(i):
+        nat.check(L.xhe_encode_f64(dk.handle, x.data_ptr(), N, 7, 0, 0, m.data_ptr(), ex.data_ptr(),
+                                   st.data_ptr(), stream), "encode")
+        nat.check(L.xhe_rand(dk.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
+        nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, ct)
+
+    for i in range(args.warmup):
+        step(1_000_000 + i)
+    torch.cuda.synchronize()
+    # parity spot check of this rank's output against the oracle (not timed)
+    from oracle import paillier_oracle as O
+    okey = O.derive_private(p, q, h)
+    idx = [0, 1, N // 2, N - 1]
+    xs = x[idx].cpu().numpy()
+    cts = nat.words_to_ints(ct[idx].cpu().numpy().view(np.uint32))
+    rs = nat.words_to_ints(rnd[idx].cpu().numpy().view(np.uint32))
+    parity_ok = all(O.encrypt_m(okey, O.encode_element(okey, float(xv), 7)[0], rv) == cv
+                    for xv, rv, cv in zip(xs, rs, cts))
+
+    L.xhe_profile(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.time()
+    ev0.record()
+    for i in range(args.steps):
+        step(i)
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.time() - t0
+    ms_total = ev0.elapsed_time(ev1)
+    tot = __import__("ctypes").c_double()
+    cnt = __import__("ctypes").c_int64()
+    nat.check(L.xhe_profile_read(b"k_djn_pow", __import__("ctypes").byref(tot), __import__("ctypes").byref(cnt)))
+    L.xhe_profile(0)
+    elapsed = max(wall, ms_total / 1e3)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ok = torch.tensor([1 if parity_ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity_ok = bool(ok.item())
+
+    value = world * N * args.steps / elapsed
+    if rank == 0:
+        w_elem, w_pow = algorithmic_macs_per_element(bits, args.win, dk.rand_bits)
+        pow_avg_s = (tot.value / max(cnt.value, 1)) / 1e3
+        achieved = N * w_pow / pow_avg_s / 1e12  # k_djn_pow: N elements x 2 primes per launch
+        rec = {
+            "metric": "2048-bit Paillier encrypts/s (device-resident)" if bits == 2048 else f"{bits}-bit Paillier encrypts/s (device-resident)",
+            "value": value, "unit": "encrypts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"DJN private-key (CRT) encrypt, obfuscated, precision 7, {N} float64 "
+                                   f"plaintexts/GPU resident in HBM" + (", + RCCL all-gather" if world > 1 else ""),
+                       "key_bits": bits, "elements_per_gpu": N, "fixed_base_window_bits": args.win,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "valu-int", "achieved": achieved, "peak": PEAK_MAC_PER_S / 1e12,
+                         "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": None,
+                         "kernel": "k_djn_pow", "kernel_avg_ms": pow_avg_s * 1e3,
+                         "alg_macs_per_element": w_pow},
+            "parity_sample_ok": parity_ok,
+            "key_setup_s": t_key,
+        }
+        if not args.no_cpu_baseline:
+            cores = min(os.cpu_count() or 1, 16)
+            rec["cpu_baseline"] = cpu_baseline(bits, args.cpu_seconds, cores)
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

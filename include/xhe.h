@@ -72,6 +72,13 @@ int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev
 int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct);
 int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint32_t* m);
 
+/* Kernel timing: when enabled, the library brackets each launch of its
+ * dominant kernels (k_djn_pow, k_dec_pow) with hipEvents on the launch stream.
+ * xhe_profile(1) enables and clears, xhe_profile(0) disables and clears;
+ * xhe_profile_read sums the recorded durations of `kernel` (NULL = all). */
+int xhe_profile(int enable);
+int xhe_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+
 int xhe_device_count(void);
 int xhe_synchronize(void* stream);
 const char* xhe_last_error(void);

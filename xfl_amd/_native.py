@@ -41,6 +41,9 @@ SIGNATURES = {
     "xhe_decode": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
     "xhe_encrypt_host": (ctypes.c_int, [_vp, _u32p, _u32p, ctypes.c_int64, _u32p]),
     "xhe_decrypt_host": (ctypes.c_int, [_vp, _u32p, ctypes.c_int64, _u32p]),
+    "xhe_profile": (ctypes.c_int, [ctypes.c_int]),
+    "xhe_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int64)]),
     "xhe_device_count": (ctypes.c_int, []),
     "xhe_synchronize": (ctypes.c_int, [_vp]),
     "xhe_last_error": (ctypes.c_char_p, []),

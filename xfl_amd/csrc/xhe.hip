@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -271,6 +272,39 @@ int blocks_for(int64_t count, int tpi, int cap) {
 
 constexpr int64_t kChunk = 1 << 20;  // elements per launch chunk (bounds workspace)
 
+// ---- optional per-kernel timing (hipEvents on the launch stream)
+struct ProfRec {
+  std::string name;
+  hipEvent_t a, b;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+
+struct ProfScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t s;
+  const char* name;
+  bool on;
+  ProfScope(const char* n, hipStream_t st) : s(st), name(n) {
+    {
+      std::lock_guard<std::mutex> lk(g_prof_mu);
+      on = g_prof_on;
+    }
+    if (on) {
+      HIPCHK(hipEventCreate(&a));
+      HIPCHK(hipEventCreate(&b));
+      HIPCHK(hipEventRecord(a, s));
+    }
+  }
+  ~ProfScope() {
+    if (!on) return;
+    if (hipEventRecord(b, s) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof.push_back({name, a, b});
+  }
+};
+
 template <class Sh>
 void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -280,9 +314,12 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
-    hipLaunchKernelGGL(k_djn_pow<MP2>, dim3(blocks, 2), dim3(256), 0, s, k->kd, m + (size_t)off * k->nw,
-                       r + (size_t)off * k->rand_words, k->rand_words, n, ws);
-    HIPCHK(hipGetLastError());
+    {
+      ProfScope ps("k_djn_pow", s);
+      hipLaunchKernelGGL(k_djn_pow<MP2>, dim3(blocks, 2), dim3(256), 0, s, k->kd, m + (size_t)off * k->nw,
+                         r + (size_t)off * k->rand_words, k->rand_words, n, ws);
+      HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, n, ws, ct + (size_t)off * k->n2w);
     HIPCHK(hipGetLastError());
   }
@@ -302,9 +339,12 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
   HIPCHK(hipMallocAsync((void**)&mrows, (size_t)2 * 2 * MP::S4 * chunk * sizeof(uint32_t), s));
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
-    hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, ct + (size_t)off * k->n2w, n,
-                       xrows, ws);
-    HIPCHK(hipGetLastError());
+    {
+      ProfScope ps("k_dec_pow", s);
+      hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, ct + (size_t)off * k->n2w, n,
+                         xrows, ws);
+      HIPCHK(hipGetLastError());
+    }
     int blocks = (int)((n * MP::TPI + 255) / 256);
     hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, n, xrows, mrows);
     HIPCHK(hipGetLastError());
@@ -525,6 +565,34 @@ int xhe_device_count(void) {
 int xhe_synchronize(void* stream) {
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e != hipSuccess) return fail(XHE_EHIP, hipGetErrorString(e));
+  return XHE_OK;
+}
+
+int xhe_profile(int enable) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = enable != 0;
+  for (auto& r : g_prof) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  g_prof.clear();
+  return XHE_OK;
+}
+
+int xhe_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  double t = 0;
+  int64_t n = 0;
+  for (auto& r : g_prof) {
+    if (kernel && r.name != kernel) continue;
+    if (hipEventSynchronize(r.b) != hipSuccess) return fail(XHE_EHIP, "xhe_profile_read: event sync failed");
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return fail(XHE_EHIP, "xhe_profile_read: elapsed failed");
+    t += ms;
+    ++n;
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = n;
   return XHE_OK;
 }
 
