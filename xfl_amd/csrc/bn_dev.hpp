@@ -149,12 +149,7 @@ struct Mont {
   uint32_t nl[TPI_ == 1 ? 1 : L];  // this lane's modulus limbs (TPI > 1)
 
   XHE_DEV void init(const uint32_t* Np, uint32_t ninv) {
-    // N + opaque 0: same provenance (keeps noalias, so limb loads stay scalar
-    // s_loads) but the loads cannot be hoisted above this point. Limbs are
-    // then held in SGPRs only while this Mont object is in use.
-    int z;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    N = Np + z;
+    N = Np;
     n0inv = ninv;
     if constexpr (TPI > 1) {
       const int g = G::g();
@@ -173,14 +168,52 @@ struct Mont {
     else return mad64(m, nl[j], c);
   }
 
+  // T[j-1+k] = T[j+k] + ai*b[j+k] + m*N[j+k], k = 0..3, in place: the block
+  // writes T[j-1] first (its old value is already consumed), then T[j] from
+  // T[j+1], ... so T[j-1..j+2] are tied in/out operands and each accumulator
+  // keeps its register across steps (no rotation copies at the loop edge).
+  XHE_DEV void mac4(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, uint32_t m,
+                    int j) const {
+#define XHE_MAC4_ASM                        \
+  "v_mad_u64_u32 %0, vcc, %5, %7, %1\n\t"   \
+  "v_mad_u64_u32 %0, vcc, %6, %11, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %5, %8, %2\n\t"   \
+  "v_mad_u64_u32 %1, vcc, %6, %12, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %5, %9, %3\n\t"   \
+  "v_mad_u64_u32 %2, vcc, %6, %13, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %5, %10, %4\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %6, %14, %3"
+    if constexpr (TPI == 1) {
+      asm(XHE_MAC4_ASM
+          : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2])
+          : "v"(T[j + 3]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]),
+            "s"(Np[j]), "s"(Np[j + 1]), "s"(Np[j + 2]), "s"(Np[j + 3])
+          : "vcc");
+    } else {
+      asm(XHE_MAC4_ASM
+          : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2])
+          : "v"(T[j + 3]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]),
+            "v"(nl[j]), "v"(nl[j + 1]), "v"(nl[j + 2]), "v"(nl[j + 3])
+          : "vcc");
+    }
+#undef XHE_MAC4_ASM
+  }
+
   // One column of the product: T <- (T + a_i*b + m*N) / 2^W
   XHE_DEV void step(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, bool lead) const {
     uint64_t x0 = mad64(ai, b[0], T[0]);
     uint32_t m = ((uint32_t)x0 * n0inv) & MASK;
     m = G::bcast0(m);
     x0 = madN(Np, m, 0, x0);
+    // 4 limbs (8 mads) per asm statement: hipcc separates inline-asm
+    // statements with s_nop, so one statement per mad would cost an issue slot
+    // per mad. Outputs are early-clobber so T[j-1] can reuse its own dead
+    // register (no register rotation / back-edge copies).
+    int j = 1;
 #pragma unroll
-    for (int j = 1; j < L; ++j) T[j - 1] = madN(Np, m, j, mad64(ai, b[j], T[j]));
+    for (; j + 4 <= L; j += 4) mac4(Np, T, b, ai, m, j);
+#pragma unroll
+    for (; j < L; ++j) T[j - 1] = madN(Np, m, j, mad64(ai, b[j], T[j]));
     T[L - 1] = G::from_next64(x0);
     T[0] += lead ? (x0 >> W) : 0ull;
   }

@@ -215,8 +215,12 @@ XHE_DEV void fixed_base_pow(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t*
 //   c   = c_q + q^2 ((c_p + 4p^2 - c_q) (q^2)^-1 mod p^2)    k_crt_enc
 // Element rows live in ws as [prime][2*S4 limbs][count] (limb i of element e
 // at row[i * count + e]); the second half of each row is wide-product scratch.
+// Np2/Nq2: the p^2 / q^2 limb rows passed as separate noalias arguments so
+// the modulus limbs are provably read-only and stay in SGPRs (scalar loads).
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* __restrict__ m_words,
+__global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* __restrict__ Np2,
+                                                    const uint32_t* __restrict__ Nq2,
+                                                    const uint32_t* __restrict__ m_words,
                                                     const uint32_t* __restrict__ a_words, int aw, int64_t count,
                                                     uint32_t* __restrict__ ws) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
@@ -225,7 +229,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   const ModDev& md = prime ? key.q2 : key.p2;
   const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
   MP2 M;
-  M.init(md.N, md.n0inv);
+  M.init(prime ? Nq2 : Np2, md.n0inv);
   uint32_t b[MP2::L];
   M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
   M.mul(b, ARow{prime ? key.nR2_q2 : key.nR2_p2});  // n m R mod P^2
