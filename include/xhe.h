@@ -68,7 +68,39 @@ int xhe_decrypt(const xhe_key* key, const uint32_t* ct_dev, int64_t count, uint3
 int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev, int64_t count, double* f64_dev,
                float* f32_dev, int32_t* status_dev, void* stream);
 
+/* Ciphertext addition PaillierCiphertext._add_encrypted (paillier.py:106-123,
+ * 79-86, 153-154): out = a' * b' mod n^2 where the operand with the larger
+ * exponent is first raised to 2^(e - min(ea, eb)); eout = min(ea, eb).
+ * ea/eb may be NULL (all 0). dmax >= max |ea - eb| bounds the squarings. */
+int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev, const uint32_t* b_dev,
+               const int32_t* eb_dev, int64_t count, int dmax, uint32_t* out_dev, int32_t* eout_dev, void* stream);
+/* PaillierCiphertext._raw_mul positive branch (paillier.py:156-187):
+ * out = c^k mod n^2, k per element (kw words, k < 2^kbits). */
+int xhe_powmod(const xhe_key* key, const uint32_t* c_dev, const uint32_t* k_dev, int kw, int kbits, int64_t count,
+               uint32_t* out_dev, void* stream);
+/* utils.invert over n^2 (utils.py:71-76) for a batch: out = c^-1 mod n^2
+ * (product-tree batch inversion). XHE_ENOINV when some c has no inverse. */
+int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_t* out_dev, void* stream);
+
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
+int xhe_mulmod_host(const xhe_key* key, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
+                    int64_t count, int dmax, uint32_t* out, int32_t* eout);
+/* c^k (or (c^-1)^k when invert_first: the negative-scalar branch). */
+int xhe_powmod_host(const xhe_key* key, const uint32_t* c, const uint32_t* k, int kw, int kbits, int64_t count,
+                    int invert_first, uint32_t* out);
+/* Paillier.encrypt over a float64 array (paillier.py:289-339): encode + (device
+ * ChaCha20 randomness when obfuscate) + encrypt; ct, exponent and encode
+ * status per element. */
+int xhe_encrypt_f64_host(const xhe_key* key, const double* x, int64_t count, int precision, int has_max,
+                         int max_exponent, int obfuscate, const uint8_t* seed32, uint64_t nonce, uint32_t* ct,
+                         int32_t* exps, int32_t* status);
+/* Paillier.encrypt of already-encoded integers m (nw words each). */
+int xhe_encrypt_words_host(const xhe_key* key, const uint32_t* m, int64_t count, int obfuscate,
+                           const uint8_t* seed32, uint64_t nonce, uint32_t* ct);
+/* Paillier.decrypt(dtype='float') (paillier.py:370-398): decrypt + decode;
+ * m_out (nullable) receives the encoded integers. */
+int xhe_decrypt_decode_host(const xhe_key* key, const uint32_t* ct, const int32_t* exps, int64_t count, double* f64,
+                            float* f32, int32_t* status, uint32_t* m_out);
 int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct);
 int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint32_t* m);
 

@@ -1,0 +1,185 @@
+"""The drop-in package (xfl_amd.paillier) against the reference's outputs.
+
+Homomorphic operations are checked bit-exactly against the golden vectors
+(tests/golden, produced by XFL's own code); randomized encryption is checked
+through decryption, with the same tolerances as the reference's tests
+(test/common/crypto/paillier/test_paillier.py).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import FIXTURES, fl, hx, load_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctxs(g):
+    from xfl_amd.paillier import PaillierContext
+    k = g["key"]
+    h = hx(k["h_pow_n"]) if k["djn_on"] else None
+    priv = PaillierContext().init(hx(k["p"]), hx(k["q"]), djn_h_pow_n=h)
+    return priv, priv.to_public()
+
+
+def _cts(ctx, d):
+    from xfl_amd.paillier import PaillierCiphertext
+    return np.array([PaillierCiphertext(ctx, hx(r), e) for r, e in zip(d["raw"], d["exp"])], dtype=object)
+
+
+def _raw(arr):
+    return [c.raw_ciphertext for c in np.asarray(arr, dtype=object).reshape(-1)], \
+        [c.exponent for c in np.asarray(arr, dtype=object).reshape(-1)]
+
+
+@pytest.mark.parametrize("fx", FIXTURES[:2])
+def test_ops_bit_exact(fx):
+    g = load_fixture(fx)
+    priv, pub = _ctxs(g)
+    ops = g["ops"]
+    a = _cts(pub, ops["a"])
+    b = _cts(pub, ops["b"])
+    sc = [fl(s) if isinstance(s, str) else s for s in ops["mul_pub"]["scalar"]]
+    want = lambda name: ([hx(r) for r in ops[name]["raw"]], ops[name]["exp"])  # noqa: E731
+    assert _raw(a + b) == want("add")
+    assert _raw(a - b) == want("sub")
+    assert _raw(np.array([a[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_pub")
+    a_priv = _cts(priv, ops["a"])
+    assert _raw(np.array([a_priv[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_priv")
+    assert _raw(np.array([a[i] + sc[i] for i in range(len(a))], dtype=object)) == want("add_scalar")
+    assert _raw(np.array([sc[i] - a[i] for i in range(len(a))], dtype=object)) == want("rsub_scalar")
+    assert _raw(a / 4.0) == want("truediv")
+    assert _raw(np.array([np.sum(a)], dtype=object)) == want("sum_a")
+    assert _raw(np.array([sum(a)], dtype=object)) == want("sum_pyfold")
+    X = np.array([[fl(v) for v in row] for row in ops["matmul"]["X"]], dtype=np.float32)
+    assert _raw(np.matmul(a, X)) == want("matmul")
+
+
+def test_histogram_groupby_bit_exact():
+    import pandas as pd
+    g = load_fixture(FIXTURES[0])
+    priv, pub = _ctxs(g)
+    h = g["ops"]["hist"]
+    c = _cts(pub, h["ct"])
+    df = pd.DataFrame({"bin": h["bins"], "xfl_grad_hess": c})
+    agg = df.groupby(["bin"])["xfl_grad_hess"].agg(["count", "sum"])
+    assert list(agg["count"]) == h["count"]
+    assert _raw(np.array(list(agg["sum"]), dtype=object)) == ([hx(r) for r in h["sum"]["raw"]], h["sum"]["exp"])
+
+
+@pytest.mark.parametrize("fx", FIXTURES)
+def test_decrypt_matches_reference(fx):
+    from xfl_amd.paillier import Paillier
+    g = load_fixture(fx)
+    priv, pub = _ctxs(g)
+    for case in ("priv_f32_p7", "pub_f64_none_max-60", "priv_packed_p0"):
+        enc = g["encrypt"][case]
+        dec = g["decrypt"][case]
+        c = _cts(priv, enc)
+        f32 = Paillier.decrypt(priv, c, dtype="float", num_cores=1)
+        assert [float(v).hex() for v in f32.astype(np.float64)] == dec["float32"]
+        org = Paillier.decrypt(priv, c, num_cores=1, out_origin=True)
+        for v, want in zip(org, dec["origin_f64"]):
+            assert (float(v).hex() if isinstance(v, float) else float(v).hex()) == want or isinstance(v, int)
+
+
+def test_wire_roundtrip_with_reference_pickles():
+    from xfl_amd.paillier import Paillier, PaillierContext
+    g = load_fixture(FIXTURES[0])
+    priv, pub = _ctxs(g)
+    ctx = PaillierContext.deserialize_from(bytes.fromhex(g["ops"]["wire_ctx_pub"]))
+    assert ctx.n == pub.n
+    arr = Paillier.ciphertext_from(None, bytes.fromhex(g["ops"]["wire_a4"]), compression=False)
+    assert [c.raw_ciphertext for c in arr] == [hx(r) for r in g["ops"]["a"]["raw"][:4]]
+    back = Paillier.ciphertext_from(priv, Paillier.serialize(arr, compression=True), compression=True)
+    assert [c.raw_ciphertext for c in back] == [c.raw_ciphertext for c in arr]
+
+
+# ---- ports of the reference's tolerance tests (test_paillier.py:24-296)
+data = [(True, None, True, -1), (True, 7, True, -1), (True, 7, False, 1),
+        (False, None, True, -1), (False, 7, True, -1), (False, 7, False, 1)]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from xfl_amd.paillier import PaillierContext
+    return PaillierContext.generate(2048)
+
+
+@pytest.mark.parametrize("djn_on, precision, is_batch, num_cores", data)
+def test_unary(ctx, djn_on, precision, is_batch, num_cores):
+    from xfl_amd.paillier import Paillier
+    p1 = np.random.random((50,)).astype(np.float32) * 100 - 50 if is_batch else random.random() * 100 - 50
+    c1 = Paillier.encrypt(ctx, p1, precision=precision, max_exponent=None, obfuscation=True, num_cores=num_cores)
+    pub = ctx.to_public()
+    c11 = Paillier.encrypt(pub, p1, precision=precision, max_exponent=None, obfuscation=True, num_cores=num_cores)
+    a = Paillier.decrypt(ctx, c1, num_cores=num_cores)
+    assert np.all(np.abs(a - p1) < 1e-4)
+    b = Paillier.decrypt(ctx, c11, num_cores=num_cores)
+    assert np.all(np.abs(b - p1) < 1e-4)
+    with pytest.raises(TypeError):
+        Paillier.decrypt(pub, c1, num_cores=num_cores)
+
+
+@pytest.mark.parametrize("djn_on, precision, is_batch, num_cores", data)
+def test_binary(ctx, djn_on, precision, is_batch, num_cores):
+    from xfl_amd.paillier import Paillier
+    if is_batch:
+        p1 = np.random.random((50,)).astype(np.float32) * 100 - 50
+        p2 = np.random.random((50,)).astype(np.float32) * 100 - 20
+    else:
+        p1 = random.random() * 100 - 50
+        p2 = random.random() * 100 - 20
+    c1 = Paillier.encrypt(ctx, p1, precision=precision, obfuscation=True, num_cores=num_cores)
+    c2 = Paillier.encrypt(ctx, p2, precision=precision, obfuscation=True, num_cores=num_cores)
+    eps = 1e-4
+    if is_batch:
+        assert abs(Paillier.decrypt(ctx, sum(c1)) - np.sum(p1.astype(np.float64))) < 1e-2
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 + c2) - (p1 + p2)) < eps)
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 - c2) - (p1 - p2)) < eps)
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 + p2) - (p1 + p2)) < eps)
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 - p2) - (p1 - p2)) < eps)
+    assert np.all(np.abs(Paillier.decrypt(ctx, p2 - c1) - (p2 - p1)) < eps)
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 * p2) - (p1 * p2)) < 1e-2)
+    assert np.all(np.abs(Paillier.decrypt(ctx, c1 / p2) - (p1 / p2)) < eps)
+
+
+def test_rest_errors_and_djn():
+    from xfl_amd.paillier import Paillier, PaillierCiphertext
+    context = Paillier.context(2048)
+    p1 = random.random() * 100 - 50
+    c1 = Paillier.encrypt(context, p1, precision=7, max_exponent=None, obfuscation=True)
+    for comp in (True, False):
+        s = c1.serialize(comp)
+        c2 = PaillierCiphertext.deserialize_from(context, s, comp)
+        assert c1.raw_ciphertext == c2.raw_ciphertext and c1.exponent == c2.exponent
+    with pytest.raises(TypeError):
+        c1 + "342"
+    other = Paillier.context(2048)
+    c3 = Paillier.encrypt(other, p1, precision=7)
+    with pytest.raises(ValueError):
+        c1 + c3
+    with pytest.raises(TypeError):
+        c1 * c1
+    pub = context.to_public()
+    c1 = Paillier.obfuscate(Paillier.encrypt(pub, p1, precision=7))
+    assert abs(Paillier.decrypt(context, c1) - p1) < 1e-5
+    djn = Paillier.context(2048, djn_on=True)
+    assert abs(Paillier.decrypt(djn, Paillier.encrypt(djn, p1, precision=7)) - p1) < 1e-5
+    dpub = djn.to_public()
+    assert abs(Paillier.decrypt(djn, Paillier.encrypt(dpub, p1, precision=7)) - p1) < 1e-5
+    c = Paillier.encrypt(dpub, p1, precision=7, max_exponent=20, obfuscation=False)
+    assert abs(Paillier.decrypt(djn, c, num_cores=1) - p1) < 1e-5
+    with pytest.raises(TypeError):
+        Paillier.encrypt(dpub, "123", precision=7)
+    c3 = Paillier.obfuscate(Paillier.encrypt(dpub, 3, precision=7))
+    assert Paillier.decrypt(djn, c3, dtype="int") == 3
+    p4 = np.array([2, 3], dtype=np.int32)
+    c4 = Paillier.obfuscate(Paillier.encrypt(dpub, p4, precision=7))
+    assert np.all(Paillier.decrypt(djn, c4, dtype="int") == p4)
+    assert 123 == Paillier._decrypt_single(123, djn)
+    with pytest.raises(TypeError):
+        Paillier.decrypt(djn, 123)
+    with pytest.raises(TypeError):
+        Paillier.obfuscate(123)

@@ -22,21 +22,24 @@ def _okey(g):
     return O.derive_private(hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"]) if k["djn_on"] else None)
 
 
-DJN = [f for f in FIXTURES if "nodjn" not in f]
+ENC_CASES = ["priv_f32_p7", "priv_f64_none", "priv_packed_p0", "pub_f32_p7", "pub_f64_none_max-60",
+             "pub_i32_none", "priv_edge_p7_noobf"]
 
 
-@pytest.mark.parametrize("fx", DJN)
-@pytest.mark.parametrize("case", ["priv_f32_p7", "priv_f64_none", "priv_packed_p0"])
-def test_encrypt_djn_private_bit_exact(fx, case):
+@pytest.mark.parametrize("fx", FIXTURES)
+@pytest.mark.parametrize("case", ENC_CASES)
+def test_encrypt_bit_exact(fx, case):
+    """Every encryption mode (DJN/non-DJN x private CRT/public, obfuscated or
+    not) with the reference's recorded obfuscation draws."""
     from xfl_amd._native import ints_to_words, words_to_ints
     g = load_fixture(fx)
     c = g["encrypt"][case]
-    dk = _dkey(g)
+    dk = _dkey(g, private=c["private"])
     ok = _okey(g)
     xs = [hx(v) for v in c["input"]] if c["kind"] == "int" else [float.fromhex(v) for v in c["input"]]
     ms = [O.encode_element(ok, x, c["precision"], c["max_exponent"])[0] for x in xs]
     mw = ints_to_words(ms, dk.nw)
-    rw = ints_to_words([hx(r) for r in c["rand"]], dk.rand_words)
+    rw = ints_to_words([hx(r) for r in c["rand"]], dk.rand_words) if c["obfuscation"] else None
     out = words_to_ints(dk.encrypt_words(mw, rw))
     assert out == [hx(r) for r in c["raw"]]
 

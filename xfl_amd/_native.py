@@ -39,8 +39,19 @@ SIGNATURES = {
     "xhe_encrypt": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp]),
     "xhe_decrypt": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp]),
     "xhe_decode": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
+    "xhe_mulmod": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp]),
+    "xhe_powmod": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp]),
+    "xhe_invert": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp]),
+    "xhe_mulmod_host": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
+    "xhe_powmod_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                       _vp]),
     "xhe_encrypt_host": (ctypes.c_int, [_vp, _u32p, _u32p, ctypes.c_int64, _u32p]),
     "xhe_decrypt_host": (ctypes.c_int, [_vp, _u32p, ctypes.c_int64, _u32p]),
+    "xhe_encrypt_f64_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, _vp, _vp, _vp]),
+    "xhe_encrypt_words_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p,
+                                              ctypes.c_uint64, _vp]),
+    "xhe_decrypt_decode_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
     "xhe_profile": (ctypes.c_int, [ctypes.c_int]),
     "xhe_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64)]),

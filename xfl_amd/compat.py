@@ -1,0 +1,112 @@
+"""Wire compatibility with unmodified XFL peers (paillier.py:66-77,244-271).
+
+* Pickles name `common.crypto.paillier.paillier.RawCiphertext`, as the
+  reference's do; that module path is registered as an alias of
+  xfl_amd.paillier.paillier unless a real XFL package is already importable.
+* Reference pickles carry gmpy2 mpz values (`gmpy2.from_binary`); gmpy2 is not
+  required here — `loads` maps that global to a decoder of gmpy2's binary
+  format (b'\\x01' + sign byte + little-endian magnitude). Values we emit are
+  Python ints, which the reference's gmpy2 arithmetic accepts unchanged.
+* `compression=True` is zstd (the reference's `zstd.compress`), implemented
+  with the system libzstd through ctypes (standard frames, level 3).
+"""
+import ctypes
+import ctypes.util
+import io
+import pickle
+import sys
+import types
+
+_REF_MOD = "common.crypto.paillier.paillier"
+
+
+def _register_alias():
+    from .paillier import paillier as mod
+    if _REF_MOD in sys.modules:
+        return
+    try:  # a real XFL install wins
+        __import__(_REF_MOD)
+        return
+    except Exception:
+        pass
+    for name in ("common", "common.crypto", "common.crypto.paillier"):
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            m.__path__ = []
+            sys.modules[name] = m
+    sys.modules[_REF_MOD] = mod
+
+
+def gmpy2_from_binary(b):
+    """Decode gmpy2.to_binary(mpz) (type byte 0x01, sign 0x01/0x02)."""
+    b = bytes(b)
+    if len(b) < 2 or b[0] != 0x01:
+        raise pickle.UnpicklingError("unsupported gmpy2 binary object")
+    mag = int.from_bytes(b[2:], "little")
+    return -mag if b[1] == 0x02 else mag
+
+
+class _Unpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if module == "gmpy2" and name in ("from_binary", "_mpmath_create"):
+            if name == "from_binary":
+                return gmpy2_from_binary
+        if module == _REF_MOD and name == "RawCiphertext":
+            from .paillier.paillier import RawCiphertext
+            return RawCiphertext
+        return super().find_class(module, name)
+
+
+def dumps(obj) -> bytes:
+    _register_alias()
+    return pickle.dumps(obj)
+
+
+def loads(data: bytes):
+    _register_alias()
+    return _Unpickler(io.BytesIO(data)).load()
+
+
+# ------------------------------------------------------------------ zstd
+_zstd = None
+
+
+def _lib():
+    global _zstd
+    if _zstd is None:
+        path = ctypes.util.find_library("zstd") or "libzstd.so.1"
+        L = ctypes.CDLL(path)
+        L.ZSTD_compressBound.restype = ctypes.c_size_t
+        L.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+        L.ZSTD_compress.restype = ctypes.c_size_t
+        L.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.ZSTD_decompress.restype = ctypes.c_size_t
+        L.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.ZSTD_getFrameContentSize.restype = ctypes.c_ulonglong
+        L.ZSTD_getFrameContentSize.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.ZSTD_isError.restype = ctypes.c_uint
+        L.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        _zstd = L
+    return _zstd
+
+
+def compress(data: bytes, level: int = 3) -> bytes:
+    L = _lib()
+    cap = L.ZSTD_compressBound(len(data))
+    dst = ctypes.create_string_buffer(cap)
+    n = L.ZSTD_compress(dst, cap, data, len(data), level)
+    if L.ZSTD_isError(n):
+        raise RuntimeError("zstd compression failed")
+    return dst.raw[:n]
+
+
+def decompress(data: bytes) -> bytes:
+    L = _lib()
+    size = L.ZSTD_getFrameContentSize(data, len(data))
+    if size >= (1 << 63):  # unknown / error
+        raise RuntimeError("zstd frame without content size")
+    dst = ctypes.create_string_buffer(max(int(size), 1))
+    n = L.ZSTD_decompress(dst, int(size), data, len(data))
+    if L.ZSTD_isError(n):
+        raise RuntimeError("zstd decompression failed")
+    return dst.raw[:n]

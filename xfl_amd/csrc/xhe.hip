@@ -40,10 +40,12 @@ struct HipError : std::runtime_error {
 struct Shape2048 {
   using MP2 = Mont<74, 28, 1>;
   using MP = Mont<37, 28, 1>;
+  using MN2 = Mont<152, 27, 4>;
 };
 struct Shape3072 {
   using MP2 = Mont<110, 28, 2>;
   using MP = Mont<56, 28, 2>;
+  using MN2 = Mont<228, 27, 4>;
 };
 
 struct ModSpec {
@@ -96,7 +98,7 @@ struct xhe_key {
   int K = 0, nw = 0, n2w = 0;
   bool priv = false, djn = false;
   int rand_bits = 0, rand_words = 0;
-  ModSpec mp2{}, mp{};
+  ModSpec mp2{}, mp{}, mn2{};
   uint32_t* d_blob = nullptr;
   uint32_t* d_tab = nullptr;
   KeyDev kd{};
@@ -116,9 +118,16 @@ struct DevGuard {
   }
 };
 
+template <class MP2>
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s);
+
 template <class Sh>
 void build_tables(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s) {
-  using MP2 = typename Sh::MP2;
+  build_tables_m<typename Sh::MP2>(k, md, d_hM, d_tab, s);
+}
+
+template <class MP2>
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s) {
   uint32_t* d_ws = nullptr;
   HIPCHK(hipMalloc(&d_ws, MP2::S4 * sizeof(uint32_t) * 4));
   hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, k->kd.win, k->kd.nwin, d_tab, d_ws);
@@ -146,6 +155,14 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   minneg = sub(n, maxpos);
   size_t o_maxpos = bl.put_words(maxpos, k->nw);
   size_t o_minneg = bl.put_words(minneg, k->nw);
+  size_t o_nlim = bl.put_limbs(n, k->mp2);
+  ModOff o_n2m = put_mod(bl, n2, k->mn2);
+  size_t o_nR2n2, o_hMn2 = 0;
+  {
+    BigU Rn2 = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
+    o_nR2n2 = bl.put_limbs(mulmod(n, mulmod(Rn2, Rn2, n2), n2), k->mn2);
+    if (h && !p) o_hMn2 = bl.put_limbs(mulmod(mod(*h, n2), Rn2, n2), k->mn2);  // public DJN table base
+  }
   // randomness bound (paillier.py:195 djn_exp_bound = 2^(bitlen(n)//2); :215 r < n)
   k->rand_bits = k->djn ? (int)(n.bits() / 2) : (int)n.bits();
   k->rand_words = (k->rand_bits + 31) / 32;
@@ -154,8 +171,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     ModOff p2, q2, p, q;
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
+    size_t ep = 0, eq = 0;
   } o;
-  int pm1_bits = 0, qm1_bits = 0;
+  int pm1_bits = 0, qm1_bits = 0, ep_bits = 0, eq_bits = 0;
   if (k->priv) {
     const BigU &P = *p, &Q = *q;
     BigU p2 = mul(P, P), q2 = mul(Q, Q);
@@ -204,6 +222,12 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o.q_lim = bl.put_limbs(Q, s1);
     o.p2x = bl.put_limbs(shl(P, 1), s1);
     o.p_lim = bl.put_limbs(P, s1);
+    // non-DJN private obfuscation exponents ep = n mod phi(p^2) (context.py:51-52)
+    BigU ep = mod(n, mul(P, sub(P, BigU(1)))), eq = mod(n, mul(Q, sub(Q, BigU(1))));
+    ep_bits = (int)ep.bits();
+    eq_bits = (int)eq.bits();
+    o.ep = bl.put_words(ep, k->nw);
+    o.eq = bl.put_words(eq, k->nw);
   }
   // upload
   HIPCHK(hipMalloc(&k->d_blob, bl.h.size() * sizeof(uint32_t)));
@@ -219,6 +243,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   kd.n2_words = B + o_n2;
   kd.maxpos = B + o_maxpos;
   kd.minneg = B + o_minneg;
+  kd.n_lim = B + o_nlim;
+  kd.n2 = moddev(B, o_n2m);
+  kd.nR2_n2 = B + o_nR2n2;
+  kd.n_bits = (int)n.bits();
   if (k->priv) {
     kd.p2 = moddev(B, o.p2);
     kd.q2 = moddev(B, o.q2);
@@ -241,6 +269,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.q_lim = B + o.q_lim;
     kd.p2x_lim = B + o.p2x;
     kd.p_lim = B + o.p_lim;
+    kd.ep_words = B + o.ep;
+    kd.eq_words = B + o.eq;
+    kd.ep_bits = ep_bits;
+    kd.eq_bits = eq_bits;
     if (k->djn) {
       kd.win = win;
       kd.nwin = (k->rand_bits + win - 1) / win;
@@ -260,6 +292,19 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       }
       HIPCHK(hipStreamDestroy(s));
     }
+  }
+  if (!k->priv && k->djn) {
+    kd.win = win;
+    kd.nwin = (k->rand_bits + win - 1) / win;
+    size_t rows = (size_t)kd.nwin << win;
+    size_t tab_words = rows * k->mn2.S4();
+    HIPCHK(hipMalloc(&k->d_tab, tab_words * sizeof(uint32_t)));
+    kd.tab_n2 = k->d_tab;
+    hipStream_t s;
+    HIPCHK(hipStreamCreate(&s));
+    if (K == 2048) build_tables_m<Shape2048::MN2>(k, kd.n2, B + o_hMn2, k->d_tab, s);
+    else build_tables_m<Shape3072::MN2>(k, kd.n2, B + o_hMn2, k->d_tab, s);
+    HIPCHK(hipStreamDestroy(s));
   }
 }
 
@@ -327,6 +372,178 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   HIPCHK(hipFreeAsync(ws, s));
 }
 
+// grid for per-group-workspace (grid-stride) kernels
+template <class M_>
+int pow_grid(int64_t count, int cap_blocks) {
+  return (int)std::min<int64_t>((count * M_::TPI + 255) / 256, cap_blocks);
+}
+
+template <class Sh>
+void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
+                          hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)MN2::S4 * chunk * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    int blocks = (int)((n * MN2::TPI + 255) / 256);
+    ProfScope ps("k_djn_pub", s);
+    hipLaunchKernelGGL(k_djn_pub<MN2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.n2.N, m + (size_t)off * k->nw,
+                       r + (size_t)off * k->rand_words, k->rand_words, n, ws, ct + (size_t)off * k->n2w);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
+
+template <class Sh>
+void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
+                        hipStream_t s) {
+  if (k->priv) {
+    using MP2 = typename Sh::MP2;
+    int64_t chunk = std::min<int64_t>(count, kChunk);
+    int pb = pow_grid<MP2>(chunk, 512);
+    int64_t groups = (int64_t)pb * 256 / MP2::TPI;
+    uint32_t *ws = nullptr, *rows = nullptr;
+    HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 18 * MP2::S4 * groups * sizeof(uint32_t), s));
+    HIPCHK(hipMallocAsync((void**)&rows, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+    for (int64_t off = 0; off < count; off += chunk) {
+      int64_t n = std::min(chunk, count - off);
+      {
+        ProfScope ps("k_nodjn_crt", s);
+        hipLaunchKernelGGL(k_nodjn_crt<MP2>, dim3(pb, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
+                           m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, rows, ws);
+        HIPCHK(hipGetLastError());
+      }
+      int blocks = (int)((n * MP2::TPI + 255) / 256);
+      hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, n, rows, ct + (size_t)off * k->n2w);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipFreeAsync(ws, s));
+    HIPCHK(hipFreeAsync(rows, s));
+  } else {
+    using MN2 = typename Sh::MN2;
+    int64_t chunk = std::min<int64_t>(count, kChunk);
+    int pb = pow_grid<MN2>(chunk, 512);
+    int64_t groups = (int64_t)pb * 256 / MN2::TPI;
+    uint32_t* ws = nullptr;
+    HIPCHK(hipMallocAsync((void**)&ws, (size_t)18 * MN2::S4 * groups * sizeof(uint32_t), s));
+    for (int64_t off = 0; off < count; off += chunk) {
+      int64_t n = std::min(chunk, count - off);
+      ProfScope ps("k_nodjn_pub", s);
+      hipLaunchKernelGGL(k_nodjn_pub<MN2>, dim3(pb), dim3(256), 0, s, k->kd, k->kd.n2.N, m + (size_t)off * k->nw,
+                         r + (size_t)off * k->rand_words, k->rand_words, n, ct + (size_t)off * k->n2w, ws);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipFreeAsync(ws, s));
+  }
+}
+
+template <class Sh>
+void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
+                 int64_t count, int dmax, uint32_t* out, int32_t* eout, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * MN2::S4 * chunk * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    int blocks = (int)((n * MN2::TPI + 255) / 256);
+    hipLaunchKernelGGL(k_mulmod_n2<MN2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.n2.N, a + (size_t)off * k->n2w,
+                       ea ? ea + off : nullptr, b + (size_t)off * k->n2w, eb ? eb + off : nullptr, n, dmax,
+                       out + (size_t)off * k->n2w, eout ? eout + off : nullptr, ws);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
+
+template <class Sh>
+void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int kw, int kbits, int64_t count,
+                 uint32_t* out, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  int pb = pow_grid<MN2>(chunk, 512);
+  int64_t groups = (int64_t)pb * 256 / MN2::TPI;
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)17 * MN2::S4 * groups * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    ProfScope ps("k_powmod_n2", s);
+    hipLaunchKernelGGL(k_powmod_n2<MN2>, dim3(pb), dim3(256), 0, s, k->kd, k->kd.n2.N, c + (size_t)off * k->n2w,
+                       kw_ + (size_t)off * kw, kw, kbits, n, out + (size_t)off * k->n2w, ws);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
+
+// Batch inversion mod n^2 via a product tree (Montgomery's trick in parallel).
+template <class Sh>
+int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* out, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  const int S4 = MN2::S4;
+  std::vector<int64_t> sizes{count};
+  while (sizes.back() > 1) sizes.push_back((sizes.back() + 1) / 2);
+  std::vector<size_t> offs;
+  size_t tot = 0;
+  for (auto n : sizes) {
+    offs.push_back(tot);
+    tot += (size_t)S4 * n;
+  }
+  uint32_t *lv = nullptr, *inv = nullptr, *scr = nullptr;
+  int32_t* st = nullptr;
+  HIPCHK(hipMallocAsync((void**)&lv, tot * 4, s));
+  HIPCHK(hipMallocAsync((void**)&inv, tot * 4, s));
+  HIPCHK(hipMallocAsync((void**)&scr, (size_t)(4 * (k->n2w + 1) + 2 * k->n2w + 8) * 4, s));
+  HIPCHK(hipMallocAsync((void**)&st, 4, s));
+  auto blocks = [&](int64_t n) { return dim3((unsigned)((n * MN2::TPI + 255) / 256)); };
+  hipLaunchKernelGGL(k_to_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, count, lv);
+  HIPCHK(hipGetLastError());
+  for (size_t l = 1; l < sizes.size(); ++l) {
+    hipLaunchKernelGGL(k_tree_up<MN2>, blocks(sizes[l]), dim3(256), 0, s, k->kd, k->kd.n2.N, lv + offs[l - 1],
+                       sizes[l - 1], lv + offs[l], sizes[l]);
+    HIPCHK(hipGetLastError());
+  }
+  size_t top = offs.back();
+  uint32_t* y_words = scr + 4 * (k->n2w + 1);
+  uint32_t* r_words = y_words + k->n2w;
+  hipLaunchKernelGGL(k_row_pack<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, lv + top, r_words);
+  hipLaunchKernelGGL(k_inv_single, dim3(1), dim3(64), 0, s, r_words, k->kd.n2_words, k->n2w, scr, y_words, st);
+  hipLaunchKernelGGL(k_inv_to_row<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, y_words, inv + top);
+  HIPCHK(hipGetLastError());
+  for (size_t l = sizes.size() - 1; l >= 1; --l) {
+    hipLaunchKernelGGL(k_tree_down<MN2>, blocks(sizes[l - 1]), dim3(256), 0, s, k->kd, k->kd.n2.N, inv + offs[l],
+                       sizes[l], lv + offs[l - 1], sizes[l - 1], inv + offs[l - 1]);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, inv, count, out);
+  HIPCHK(hipGetLastError());
+  int32_t hst = 0;
+  HIPCHK(hipMemcpyAsync(&hst, st, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(lv);
+  (void)hipFree(inv);
+  (void)hipFree(scr);
+  (void)hipFree(st);
+  if (hst != 0) return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
+  return XHE_OK;
+}
+
+template <class Sh>
+void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32_t* ct, hipStream_t s) {
+  using MP2 = typename Sh::MP2;
+  int64_t chunk = std::min<int64_t>(count, kChunk);
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+  for (int64_t off = 0; off < count; off += chunk) {
+    int64_t n = std::min(chunk, count - off);
+    int blocks = (int)((n * MP2::TPI + 255) / 256);
+    hipLaunchKernelGGL(k_raw_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, m + (size_t)off * k->nw, n, ws,
+                       ct + (size_t)off * k->n2w);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
+
 template <class Sh>
 void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -370,6 +587,24 @@ int guarded(F&& f) {
 
 }  // namespace
 
+namespace {
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf(size_t bytes, hipStream_t s) { HIPCHK(hipMallocAsync(&p, std::max<size_t>(bytes, 4), s)); }
+  ~DevBuf() { (void)hipFree(p); }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+struct Stream {
+  hipStream_t s = nullptr;
+  Stream() { HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+  ~Stream() {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+};
+}  // namespace
+
 extern "C" {
 
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
@@ -392,9 +627,11 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     if (key_bits == 2048) {
       k->mp2 = {Shape2048::MP2::S, Shape2048::MP2::W};
       k->mp = {Shape2048::MP::S, Shape2048::MP::W};
+      k->mn2 = {Shape2048::MN2::S, Shape2048::MN2::W};
     } else {
       k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
       k->mp = {Shape3072::MP::S, Shape3072::MP::W};
+      k->mn2 = {Shape3072::MN2::S, Shape3072::MN2::W};
     }
     BigU n = BigU::from_words(n_words, k->nw);
     if ((int)n.bits() > key_bits || n.bits() + 2 < (size_t)key_bits)
@@ -479,11 +716,23 @@ int xhe_encrypt(const xhe_key* key, const uint32_t* m_dev, const uint32_t* rand_
   return guarded([&]() -> int {
     if (!key || (count > 0 && (!m_dev || !ct_dev))) return fail(XHE_EINVAL, "xhe_encrypt: null argument");
     if (count <= 0) return XHE_OK;
-    if (!(key->priv && key->djn && rand_dev))
-      return fail(XHE_ENOTSUP, "xhe_encrypt: only DJN private-key obfuscated encryption is built");
     DevGuard dg(key->device);
-    if (key->K == 2048) encrypt_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, (hipStream_t)stream);
-    else encrypt_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, (hipStream_t)stream);
+    hipStream_t s = (hipStream_t)stream;
+    if (!rand_dev) {
+      if (key->K == 2048) raw_encrypt_impl<Shape2048>(key, m_dev, count, ct_dev, s);
+      else raw_encrypt_impl<Shape3072>(key, m_dev, count, ct_dev, s);
+      return XHE_OK;
+    }
+    if (key->djn && key->priv) {
+      if (key->K == 2048) encrypt_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
+      else encrypt_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+    } else if (key->djn) {
+      if (key->K == 2048) encrypt_pub_djn_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
+      else encrypt_pub_djn_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+    } else {
+      if (key->K == 2048) encrypt_nodjn_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
+      else encrypt_nodjn_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+    }
     return XHE_OK;
   });
 }
@@ -554,6 +803,172 @@ int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint
     if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
     if (count <= 0) return XHE_OK;
     return host_roundtrip(key, ct, (size_t)count * key->n2w, m, (size_t)count * key->nw, nullptr, 0, false);
+  });
+}
+
+int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev, const uint32_t* b_dev,
+               const int32_t* eb_dev, int64_t count, int dmax, uint32_t* out_dev, int32_t* eout_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!a_dev || !b_dev || !out_dev)) || dmax < 0)
+      return fail(XHE_EINVAL, "xhe_mulmod: bad argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    if (key->K == 2048) mulmod_impl<Shape2048>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, (hipStream_t)stream);
+    else mulmod_impl<Shape3072>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
+int xhe_powmod(const xhe_key* key, const uint32_t* c_dev, const uint32_t* k_dev, int kw, int kbits, int64_t count,
+               uint32_t* out_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!c_dev || !k_dev || !out_dev)) || kw <= 0 || kbits < 0 || kbits > 32 * kw)
+      return fail(XHE_EINVAL, "xhe_powmod: bad argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    if (key->K == 2048) powmod_impl<Shape2048>(key, c_dev, k_dev, kw, kbits, count, out_dev, (hipStream_t)stream);
+    else powmod_impl<Shape3072>(key, c_dev, k_dev, kw, kbits, count, out_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
+int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_t* out_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!c_dev || !out_dev))) return fail(XHE_EINVAL, "xhe_invert: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    if (key->K == 2048) return invert_impl<Shape2048>(key, c_dev, count, out_dev, (hipStream_t)stream);
+    return invert_impl<Shape3072>(key, c_dev, count, out_dev, (hipStream_t)stream);
+  });
+}
+
+
+int xhe_encrypt_f64_host(const xhe_key* key, const double* x, int64_t count, int precision, int has_max,
+                         int max_exponent, int obfuscate, const uint8_t* seed32, uint64_t nonce, uint32_t* ct,
+                         int32_t* exps, int32_t* status) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!x || !ct || !exps || !status)) || (obfuscate && !seed32))
+      return fail(XHE_EINVAL, "xhe_encrypt_f64_host: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    Stream st;
+    DevBuf dx(count * 8, st.s), dm((size_t)count * key->nw * 4, st.s), de(count * 4, st.s), ds(count * 4, st.s),
+        dc((size_t)count * key->n2w * 4, st.s), dr(obfuscate ? (size_t)count * key->rand_words * 4 : 4, st.s);
+    HIPCHK(hipMemcpyAsync(dx.p, x, count * 8, hipMemcpyHostToDevice, st.s));
+    int rc = xhe_encode_f64(key, dx.as<double>(), count, precision, has_max, max_exponent, dm.as<uint32_t>(),
+                            de.as<int32_t>(), ds.as<int32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    if (obfuscate) {
+      rc = xhe_rand(key, seed32, nonce, count, dr.as<uint32_t>(), nullptr, st.s);
+      if (rc != XHE_OK) return rc;
+    }
+    rc = xhe_encrypt(key, dm.as<uint32_t>(), obfuscate ? dr.as<uint32_t>() : nullptr, count, dc.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(ct, dc.p, (size_t)count * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipMemcpyAsync(exps, de.p, count * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipMemcpyAsync(status, ds.p, count * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_encrypt_words_host(const xhe_key* key, const uint32_t* m, int64_t count, int obfuscate,
+                           const uint8_t* seed32, uint64_t nonce, uint32_t* ct) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!m || !ct)) || (obfuscate && !seed32))
+      return fail(XHE_EINVAL, "xhe_encrypt_words_host: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    Stream st;
+    DevBuf dm((size_t)count * key->nw * 4, st.s), dc((size_t)count * key->n2w * 4, st.s),
+        dr(obfuscate ? (size_t)count * key->rand_words * 4 : 4, st.s);
+    HIPCHK(hipMemcpyAsync(dm.p, m, (size_t)count * key->nw * 4, hipMemcpyHostToDevice, st.s));
+    int rc = XHE_OK;
+    if (obfuscate) {
+      rc = xhe_rand(key, seed32, nonce, count, dr.as<uint32_t>(), nullptr, st.s);
+      if (rc != XHE_OK) return rc;
+    }
+    rc = xhe_encrypt(key, dm.as<uint32_t>(), obfuscate ? dr.as<uint32_t>() : nullptr, count, dc.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(ct, dc.p, (size_t)count * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_decrypt_decode_host(const xhe_key* key, const uint32_t* ct, const int32_t* exps, int64_t count, double* f64,
+                            float* f32, int32_t* status, uint32_t* m_out) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!ct || !exps || !f64 || !f32 || !status)))
+      return fail(XHE_EINVAL, "xhe_decrypt_decode_host: null argument");
+    if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    Stream st;
+    DevBuf dc((size_t)count * key->n2w * 4, st.s), dm((size_t)count * key->nw * 4, st.s), de(count * 4, st.s),
+        d64(count * 8, st.s), d32(count * 4, st.s), ds(count * 4, st.s);
+    HIPCHK(hipMemcpyAsync(dc.p, ct, (size_t)count * key->n2w * 4, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(de.p, exps, count * 4, hipMemcpyHostToDevice, st.s));
+    int rc = xhe_decrypt(key, dc.as<uint32_t>(), count, dm.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    rc = xhe_decode(key, dm.as<uint32_t>(), de.as<int32_t>(), count, d64.as<double>(), d32.as<float>(),
+                    ds.as<int32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(f64, d64.p, count * 8, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipMemcpyAsync(f32, d32.p, count * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipMemcpyAsync(status, ds.p, count * 4, hipMemcpyDeviceToHost, st.s));
+    if (m_out) HIPCHK(hipMemcpyAsync(m_out, dm.p, (size_t)count * key->nw * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_mulmod_host(const xhe_key* key, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
+                    int64_t count, int dmax, uint32_t* out, int32_t* eout) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!a || !b || !out))) return fail(XHE_EINVAL, "xhe_mulmod_host: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    Stream st;
+    size_t cw = (size_t)count * key->n2w * 4;
+    DevBuf da(cw, st.s), db(cw, st.s), dout(cw, st.s), dea(count * 4, st.s), deb(count * 4, st.s), deo(count * 4, st.s);
+    HIPCHK(hipMemcpyAsync(da.p, a, cw, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(db.p, b, cw, hipMemcpyHostToDevice, st.s));
+    if (ea) HIPCHK(hipMemcpyAsync(dea.p, ea, count * 4, hipMemcpyHostToDevice, st.s));
+    if (eb) HIPCHK(hipMemcpyAsync(deb.p, eb, count * 4, hipMemcpyHostToDevice, st.s));
+    int rc = xhe_mulmod(key, da.as<uint32_t>(), ea ? dea.as<int32_t>() : nullptr, db.as<uint32_t>(),
+                        eb ? deb.as<int32_t>() : nullptr, count, dmax, dout.as<uint32_t>(),
+                        eout ? deo.as<int32_t>() : nullptr, st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(out, dout.p, cw, hipMemcpyDeviceToHost, st.s));
+    if (eout) HIPCHK(hipMemcpyAsync(eout, deo.p, count * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_powmod_host(const xhe_key* key, const uint32_t* c, const uint32_t* k, int kw, int kbits, int64_t count,
+                    int invert_first, uint32_t* out) {
+  return guarded([&]() -> int {
+    if (!key || (count > 0 && (!c || !k || !out))) return fail(XHE_EINVAL, "xhe_powmod_host: null argument");
+    if (count <= 0) return XHE_OK;
+    DevGuard dg(key->device);
+    Stream st;
+    size_t cw = (size_t)count * key->n2w * 4;
+    DevBuf dc(cw, st.s), dk((size_t)count * kw * 4, st.s), dout(cw, st.s), dinv(invert_first ? cw : 4, st.s);
+    HIPCHK(hipMemcpyAsync(dc.p, c, cw, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(dk.p, k, (size_t)count * kw * 4, hipMemcpyHostToDevice, st.s));
+    const uint32_t* base = dc.as<uint32_t>();
+    if (invert_first) {
+      int rc = xhe_invert(key, dc.as<uint32_t>(), count, dinv.as<uint32_t>(), st.s);
+      if (rc != XHE_OK) return rc;
+      base = dinv.as<uint32_t>();
+    }
+    int rc = xhe_powmod(key, base, dk.as<uint32_t>(), kw, kbits, count, dout.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(out, dout.p, cw, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
   });
 }
 

@@ -29,6 +29,14 @@ struct KeyDev {
   const uint32_t* n2_words;  // n^2 (n2w words)
   const uint32_t* maxpos;    // n // 3 (nw words)
   const uint32_t* minneg;    // n - n // 3 (nw words)
+  const uint32_t* n_lim;     // n as MP2 limbs (raw encryption wide product)
+  // ---- mod n^2 (shape MN2): public-key paths and homomorphic operations
+  ModDev n2;
+  const uint32_t* nR2_n2;     // n * R^2 mod n^2
+  const uint32_t* tab_n2;     // [nwin][2^win][S4] h^(d*2^(win*w)) * R mod n^2 (public DJN)
+  const uint32_t* ep_words;   // n mod phi(p^2) (nw words), non-DJN private obfuscation exponent
+  const uint32_t* eq_words;
+  int ep_bits, eq_bits, n_bits;
   // ---- mod p^2 / q^2 (shape MP2)
   ModDev p2, q2;
   const uint32_t* nR2_p2;     // n * R^2 mod p^2
@@ -264,6 +272,28 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, int64_t count, u
   M.wide_mul_add_store(b, ARow{key.q2_lim}, rq, st, out + (size_t)e * key.n2w, key.n2w);
 }
 
+// Raw encryption without obfuscation (paillier.py:283): c = 1 + n m  (m < n,
+// so the product is already reduced mod n^2). ws: [2*S4][count] rows.
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_raw_enc(KeyDev key, const uint32_t* __restrict__ m_words, int64_t count,
+                                                    uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (e >= count) return;
+  const int st = (int)count;
+  uint32_t* row = ws + e;
+  MP2 M;
+  M.init(key.p2.N, 0);  // only the limb shape is used (no reduction)
+  uint32_t b[MP2::L];
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  {
+    const int g = MP2::G::g();
+#pragma unroll
+    for (int j = 0; j < MP2::L; ++j) row[(size_t)(g * MP2::L + j) * st] = (g == 0 && j == 0) ? 1u : 0u;
+  }
+  wave_sync_mem_();
+  M.wide_mul_add_store(b, ARow{key.n_lim}, row, st, out + (size_t)e * key.n2w, key.n2w);
+}
+
 // ---------------------------------------------------------------------------
 // Decryption (paillier.py:341-368)
 // k_dec_pow: X_P = (c^(P-1) mod P^2) - 1 for one prime (grid.y), written to
@@ -406,6 +436,391 @@ __global__ void __launch_bounds__(256, 2) k_crt_dec(KeyDev key, int64_t count, u
   M.mul(u, ARow{key.qinvpR});
   M.reduce_once(u);
   M.wide_mul_add_store(u, ARow{key.q_lim}, rq, st, m_out + (size_t)e * key.nw, key.nw);
+}
+
+// ============================================================== mod n^2
+// Helpers shared by the n^2 kernels (shape MN2, usually TPI = 4).
+template <class M_>
+XHE_DEV void store_packed(const M_& M, const uint32_t (&b)[M_::L], uint32_t* row, int st, uint32_t* out, int nwords) {
+  M.store_strided(b, row, st);
+  wave_sync_mem_();
+  pack_words_<M_::W, M_::TPI>(row, st, M_::S, out, nwords);
+}
+
+// 4-bit fixed-window power of the Montgomery residue in b. Digits come from
+// `digit(w)` (uniform inside a lane group). tab: 16 interleaved rows, sq: one.
+template <class M_, class DigitF>
+XHE_DEV void pow_window4(const M_& M, uint32_t (&b)[M_::L], const uint32_t* R1, int nwin, DigitF digit,
+                         uint32_t* tab, uint32_t* sq, int st) {
+  const size_t rs = (size_t)M_::S4 * st;
+  M.store_strided(b, tab + rs, st);  // tab[1] = b
+  {
+    uint32_t one[M_::L];
+    M.load_row(one, R1);
+    M.reduce_once(one);
+    M.store_strided(one, tab, st);   // tab[0] = R (Montgomery one)
+  }
+  wave_sync_mem_();
+  for (int t = 2; t < 16; ++t) {
+    M.mul(b, AStrided{tab + rs, st});
+    M.store_strided(b, tab + rs * t, st);
+  }
+  wave_sync_mem_();
+  M.load_strided(b, tab + rs * digit(nwin - 1), st);
+  for (int w = nwin - 2; w >= 0; --w) {
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      M.store_strided(b, sq, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq, st});
+    }
+    M.mul(b, AStrided{tab + rs * digit(w), st});
+  }
+}
+
+XHE_DEV uint32_t nibble(const uint32_t* w, int nwords, int win) {
+  int bit = win * 4;
+  int k = bit >> 5;
+  return k < nwords ? (w[k] >> (bit & 31)) & 15u : 0u;
+}
+
+// out = a * b mod n^2 after aligning exponents: the operand with the larger
+// exponent is raised to 2^(e - min(ea, eb)) first (paillier.py:79-86,106-123).
+// ws: 2 rows [2*S4][count] per element (second row = pack scratch).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                      const uint32_t* __restrict__ a, const int32_t* __restrict__ ea,
+                                                      const uint32_t* __restrict__ bw, const int32_t* __restrict__ eb,
+                                                      int64_t count, int dmax, uint32_t* __restrict__ out,
+                                                      int32_t* __restrict__ eout, uint32_t* __restrict__ ws) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (e >= count) return;
+  const int st = (int)count;
+  uint32_t* row = ws + e;
+  uint32_t* sq = ws + (size_t)MN2::S4 * count + e;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  const int e1 = ea ? ea[e] : 0, e2 = eb ? eb[e] : 0;
+  const int emin = e1 < e2 ? e1 : e2;
+  const int d1 = e1 - emin, d2 = e2 - emin;
+  uint32_t b[MN2::L];
+  // A = a R, squared d1 times, parked in `row`
+  M.load_words(b, a + (size_t)e * key.n2w, key.n2w);
+  M.mul(b, ARow{key.n2.R2});
+  for (int k = 0; k < dmax; ++k) {
+    if (k < d1) {
+      M.store_strided(b, sq, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq, st});
+    }
+  }
+  M.store_strided(b, row, st);
+  M.load_words(b, bw + (size_t)e * key.n2w, key.n2w);
+  M.mul(b, ARow{key.n2.R2});
+  for (int k = 0; k < dmax; ++k) {
+    if (k < d2) {
+      M.store_strided(b, sq, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq, st});
+    }
+  }
+  wave_sync_mem_();
+  M.mul(b, AStrided{row, st});  // A B R
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  store_packed(M, b, row, st, out + (size_t)e * key.n2w, key.n2w);
+  if (eout && MN2::G::g() == 0) eout[e] = emin;
+}
+
+// out = c^k mod n^2 with a per-element exponent k (kw words, < 2^kbits).
+// Grid-stride; per-group workspace of 17 interleaved rows (4-bit window).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_powmod_n2(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                      const uint32_t* __restrict__ c, const uint32_t* __restrict__ k,
+                                                      int kw, int kbits, int64_t count, uint32_t* __restrict__ out,
+                                                      uint32_t* __restrict__ ws) {
+  const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MN2::TPI;
+  const int64_t gid0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  const int st = (int)G_total;
+  const size_t rs = (size_t)MN2::S4 * st;
+  uint32_t* tab = ws + gid0;
+  uint32_t* sq = tab + 16 * rs;
+  const int nwin = kbits <= 0 ? 1 : (kbits + 3) / 4;
+  for (int64_t e = gid0; e < count; e += G_total) {
+    MN2 M;
+    M.init(Nn2, key.n2.n0inv);
+    uint32_t b[MN2::L];
+    M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
+    M.mul(b, ARow{key.n2.R2});
+    const uint32_t* ke = k + (size_t)e * kw;
+    pow_window4(M, b, key.n2.R1, nwin, [&](int w) { return nibble(ke, kw, w); }, tab, sq, st);
+    M.mul(b, AOne{});
+    M.reduce_once(b);
+    store_packed(M, b, sq, st, out + (size_t)e * key.n2w, key.n2w);
+  }
+}
+
+// Public-key DJN encryption (paillier.py:210-212,283): (1 + n m) h^a mod n^2
+// with the fixed-base table of h mod n^2.
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                    const uint32_t* __restrict__ m_words,
+                                                    const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                    uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (e >= count) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{key.nR2_n2});
+  M.add_row(b, key.n2.R1);
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  const int rows = 1 << key.win;
+  for (int w = 0; w < key.nwin; ++w) {
+    int bit = w * key.win;
+    uint32_t d = (ae[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    M.mul(b, ARow{key.tab_n2 + ((size_t)w * rows + d) * MN2::S4});
+  }
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  store_packed(M, b, ws + e, (int)count, out + (size_t)e * key.n2w, key.n2w);
+}
+
+// Non-DJN obfuscation, variable base r with a uniform exponent:
+//   public  (paillier.py:228-230): (1 + n m) r^n mod n^2          -> out words
+//   private (paillier.py:214-227): (1 + n m) r^e_P mod P^2, P = p/q -> ws rows
+//   for k_crt_enc (grid.y = prime).
+template <class M_>
+XHE_DEV void nodjn_core(const M_& M, uint32_t (&b)[M_::L], const ModDev& md, const uint32_t* nR2,
+                        const uint32_t* mw, int nw, const uint32_t* rw, int rwn, const uint32_t* ex, int exw,
+                        int ebits, uint32_t* tab, uint32_t* sq, uint32_t* park, int st) {
+  // c0 R = (1 + n m) R parked first
+  M.load_words(b, mw, nw);
+  M.mul(b, ARow{nR2});
+  M.add_row(b, md.R1);
+  M.store_strided(b, park, st);
+  // r R, then r^e R
+  M.load_words(b, rw, rwn);
+  M.mul(b, ARow{md.R2});
+  const int nwin = (ebits + 3) / 4;
+  pow_window4(M, b, md.R1, nwin, [&](int w) { return nibble(ex, exw, w); }, tab, sq, st);
+  wave_sync_mem_();
+  M.mul(b, AStrided{park, st});
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+}
+
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_nodjn_pub(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                      const uint32_t* __restrict__ m_words,
+                                                      const uint32_t* __restrict__ r_words, int rw, int64_t count,
+                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ ws) {
+  const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MN2::TPI;
+  const int64_t gid0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  const int st = (int)G_total;
+  const size_t rs = (size_t)MN2::S4 * st;
+  uint32_t* tab = ws + gid0;
+  for (int64_t e = gid0; e < count; e += G_total) {
+    MN2 M;
+    M.init(Nn2, key.n2.n0inv);
+    uint32_t b[MN2::L];
+    nodjn_core(M, b, key.n2, key.nR2_n2, m_words + (size_t)e * key.nw, key.nw, r_words + (size_t)e * rw, rw,
+               key.n_words, key.nw, key.n_bits, tab, tab + 16 * rs, tab + 17 * rs, st);
+    store_packed(M, b, tab + 16 * rs, st, out + (size_t)e * key.n2w, key.n2w);
+  }
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t* __restrict__ Np2,
+                                                      const uint32_t* __restrict__ Nq2,
+                                                      const uint32_t* __restrict__ m_words,
+                                                      const uint32_t* __restrict__ r_words, int rw, int64_t count,
+                                                      uint32_t* __restrict__ rows, uint32_t* __restrict__ ws) {
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MP2::TPI;
+  const int64_t gid0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  const int st = (int)G_total;
+  const size_t rs = (size_t)MP2::S4 * st;
+  uint32_t* tab = ws + (size_t)prime * 18 * rs + gid0;
+  for (int64_t e = gid0; e < count; e += G_total) {
+    MP2 M;
+    M.init(prime ? Nq2 : Np2, md.n0inv);
+    uint32_t b[MP2::L];
+    nodjn_core(M, b, md, prime ? key.nR2_q2 : key.nR2_p2, m_words + (size_t)e * key.nw, key.nw,
+               r_words + (size_t)e * rw, rw, prime ? key.eq_words : key.ep_words, key.nw,
+               prime ? key.eq_bits : key.ep_bits, tab, tab + 16 * rs, tab + 17 * rs, st);
+    M.store_strided(b, rows + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+  }
+}
+
+// ---- batch modular inversion mod n^2 (Montgomery's trick as a product tree)
+// Up-sweep: out[i] = in[2i] * in[2i+1] (Montgomery form, rows [S4][n]).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_tree_up(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                    const uint32_t* __restrict__ in, int64_t n_in,
+                                                    uint32_t* __restrict__ outp, int64_t n_out) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (i >= n_out) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_strided(b, in + 2 * i, (int)n_in);
+  if (2 * i + 1 < n_in) {
+    M.mul(b, AStrided{in + 2 * i + 1, (int)n_in});
+    M.reduce_once(b);
+  }
+  M.store_strided(b, outp + i, (int)n_out);
+}
+
+// Down-sweep: inv(child i) = inv(parent i/2) * child(i ^ 1)
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_tree_down(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                      const uint32_t* __restrict__ pinv, int64_t n_par,
+                                                      const uint32_t* __restrict__ child, int64_t n_child,
+                                                      uint32_t* __restrict__ cinv) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (i >= n_child) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_strided(b, pinv + i / 2, (int)n_par);
+  const int64_t sib = i ^ 1;
+  if (sib < n_child) {
+    M.mul(b, AStrided{child + sib, (int)n_child});
+    M.reduce_once(b);
+  }
+  M.store_strided(b, cinv + i, (int)n_child);
+}
+
+// Single modular inverse x^-1 mod m (binary extended Euclid, one lane), both
+// as nwords little-endian words; m odd. status = 1 when gcd(x, m) != 1.
+__global__ void k_inv_single(const uint32_t* __restrict__ x, const uint32_t* __restrict__ m, int nwords,
+                             uint32_t* __restrict__ scratch, uint32_t* __restrict__ out, int32_t* __restrict__ status) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const int W = nwords + 1;
+  uint32_t *u = scratch, *v = scratch + W, *x1 = scratch + 2 * W, *x2 = scratch + 3 * W;
+  for (int i = 0; i < W; ++i) {
+    u[i] = i < nwords ? x[i] : 0;
+    v[i] = i < nwords ? m[i] : 0;
+    x1[i] = i == 0 ? 1u : 0u;
+    x2[i] = 0;
+  }
+  auto is_one = [&](const uint32_t* a) {
+    if (a[0] != 1) return false;
+    for (int i = 1; i < W; ++i) if (a[i]) return false;
+    return true;
+  };
+  auto is_zero = [&](const uint32_t* a) {
+    for (int i = 0; i < W; ++i) if (a[i]) return false;
+    return true;
+  };
+  auto half = [&](uint32_t* a) {
+    for (int i = 0; i < W; ++i) a[i] = (a[i] >> 1) | (i + 1 < W ? (a[i + 1] << 31) : 0u);
+  };
+  auto add_m_half = [&](uint32_t* a) {  // a = (a + m) / 2  (a < m, so a + m < 2^(32W))
+    uint64_t c = 0;
+    for (int i = 0; i < W; ++i) {
+      c += (uint64_t)a[i] + (i < nwords ? m[i] : 0u);
+      a[i] = (uint32_t)c;
+      c >>= 32;
+    }
+    half(a);
+  };
+  auto geq = [&](const uint32_t* a, const uint32_t* b) {
+    for (int i = W - 1; i >= 0; --i) if (a[i] != b[i]) return a[i] > b[i];
+    return true;
+  };
+  auto sub_to = [&](uint32_t* a, const uint32_t* b) {  // a -= b (a >= b)
+    int64_t br = 0;
+    for (int i = 0; i < W; ++i) {
+      int64_t d = (int64_t)a[i] - b[i] - br;
+      br = d < 0;
+      a[i] = (uint32_t)(d + (br << 32));
+    }
+  };
+  auto submod_to = [&](uint32_t* a, const uint32_t* b) {  // a = (a - b) mod m, a, b < m
+    if (geq(a, b)) { sub_to(a, b); return; }
+    uint64_t c = 0;
+    for (int i = 0; i < W; ++i) {
+      c += (uint64_t)a[i] + (i < nwords ? m[i] : 0u);
+      a[i] = (uint32_t)c;
+      c >>= 32;
+    }
+    sub_to(a, b);
+  };
+  if (is_zero(u)) { status[0] = 1; return; }
+  long guard = 0;
+  while (!is_one(u) && !is_one(v)) {
+    if (++guard > 64L * 32 * W) { status[0] = 1; return; }
+    while ((u[0] & 1) == 0) {
+      half(u);
+      if (x1[0] & 1) add_m_half(x1); else half(x1);
+    }
+    while ((v[0] & 1) == 0) {
+      half(v);
+      if (x2[0] & 1) add_m_half(x2); else half(x2);
+    }
+    if (geq(u, v)) { sub_to(u, v); submod_to(x1, x2); }
+    else { sub_to(v, u); submod_to(x2, x1); }
+    if (is_zero(u) || is_zero(v)) { status[0] = 1; return; }
+  }
+  const uint32_t* r = is_one(u) ? x1 : x2;
+  for (int i = 0; i < nwords; ++i) out[i] = r[i];
+  status[0] = 0;
+}
+
+// n^2 residues (words) -> Montgomery rows [S4][count]; and back.
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_to_mont_rows(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                         const uint32_t* __restrict__ c, int64_t count,
+                                                         uint32_t* __restrict__ rows) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (e >= count) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
+  M.mul(b, ARow{key.n2.R2});
+  M.reduce_once(b);
+  M.store_strided(b, rows + e, (int)count);
+}
+
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_from_mont_rows(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                           uint32_t* __restrict__ rows, int64_t count,
+                                                           uint32_t* __restrict__ out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (e >= count) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_strided(b, rows + e, (int)count);
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  store_packed(M, b, rows + e, (int)count, out + (size_t)e * key.n2w, key.n2w);
+}
+
+// Root of the product tree <-> plain words for k_inv_single (one group).
+template <class MN2>
+__global__ void k_row_pack(KeyDev key, const uint32_t* __restrict__ Nn2, uint32_t* __restrict__ row,
+                           uint32_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x >= MN2::TPI) return;
+  pack_words_<MN2::W, MN2::TPI>(row, 1, MN2::S, out, key.n2w);
+}
+// words y = (P R)^-1 -> Montgomery row of P^-1: y * R^3 * R^-1 = P^-1 R
+template <class MN2>
+__global__ void k_inv_to_row(KeyDev key, const uint32_t* __restrict__ Nn2, const uint32_t* __restrict__ y,
+                             uint32_t* __restrict__ row) {
+  if (blockIdx.x != 0 || threadIdx.x >= MN2::TPI) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_words(b, y, key.n2w);
+  M.mul(b, ARow{key.n2.R3});
+  M.reduce_once(b);
+  M.store_row(b, row);
 }
 
 // ============================================================== tables

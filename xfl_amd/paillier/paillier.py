@@ -1,0 +1,325 @@
+"""Paillier / PaillierCiphertext / RawCiphertext — drop-in for
+python/common/crypto/paillier/paillier.py (same names, arguments, return
+types and exceptions). Arithmetic runs on the GPU (xfl_amd.paillier.ops ->
+include/xhe.h); results are bit-identical to the reference for the same keys
+and obfuscation draws (tests/test_gpu_dropin.py).
+"""
+import pickle
+import warnings
+from typing import Optional, Union
+
+import numpy as np
+
+from . import ops
+from .context import PaillierContext
+from .encoder import PaillierEncoder, int_to_float_gmpy
+from .utils import MPZ, get_core_num  # noqa: F401  (re-exported like the reference)
+
+_ST_ERR = {1: OverflowError, 2: ValueError}
+
+
+class RawCiphertext:
+    """paillier.py:39-42 — the pickled wire record (value, exp)."""
+
+    def __init__(self, value, exp):
+        self.value = value
+        self.exp = exp
+
+
+# Pickles must name the reference's module path so unmodified XFL peers can
+# load what we emit (and we can load theirs): see xfl_amd/compat.py.
+RawCiphertext.__module__ = "common.crypto.paillier.paillier"
+
+
+def _is_scalar(x):
+    return isinstance(x, (int, float)) and not isinstance(x, bool) or isinstance(x, bool)
+
+
+class PaillierCiphertext(object):
+    """paillier.py:45-232"""
+
+    def __init__(self, context: PaillierContext, raw_ciphertext: MPZ, exponent: int) -> None:
+        self.__context = context
+        self.__c = int(raw_ciphertext)
+        self.__exp = int(exponent)
+
+    @property
+    def context(self):
+        return self.__context
+
+    @property
+    def raw_ciphertext(self):
+        return self.__c
+
+    @property
+    def exponent(self):
+        return self.__exp
+
+    def serialize(self, compression: bool = True) -> bytes:
+        from ..compat import compress, dumps
+        out = dumps(RawCiphertext(self.__c, self.__exp))
+        return compress(out) if compression else out
+
+    @classmethod
+    def deserialize_from(cls, context: PaillierContext, data: bytes, compression: bool = True):
+        from ..compat import decompress, loads
+        if compression:
+            data = decompress(data)
+        r = loads(data)
+        return PaillierCiphertext(context, int(r.value), r.exp)
+
+    def _decrease_exponent_to(self, new_exponent: int):
+        """paillier.py:79-86"""
+        scalar = 1 << (self.__exp - new_exponent)
+        return ops.raw_mul(self.__context, [self.__c], [scalar])[0]
+
+    def __add__(self, other):
+        """paillier.py:88-104 (no obfuscation when adding a scalar)."""
+        if isinstance(other, PaillierCiphertext):
+            return self._add_encrypted(other)
+        elif isinstance(other, (int, float)):
+            ciphertext = Paillier.encrypt(self.context, other, precision=None, max_exponent=None, obfuscation=False)
+            return self._add_encrypted(ciphertext)
+        else:
+            raise TypeError(f"Adding data of type {type(other)} not supported.")
+
+    def _add_encrypted(self, other):
+        """paillier.py:106-123"""
+        if self.context.to_public() != other.context.to_public():
+            raise ValueError("Adding two ciphertext with different keys.")
+        r, e = ops.add(self.context, [self.__c], [self.__exp], [other.raw_ciphertext], [other.exponent])
+        return PaillierCiphertext(self.context, r[0], int(e[0]))
+
+    def __radd__(self, other):
+        return self.__add__(other)
+
+    def __sub__(self, other):
+        return self.__add__(other * (-1))
+
+    def __rsub__(self, other):
+        return ((-1) * self).__add__(other)
+
+    def __mul__(self, scalar: Union[int, float]):
+        """paillier.py:134-145"""
+        if isinstance(scalar, PaillierCiphertext):
+            raise TypeError("Cannot multiply one ciphertext with another ciphertext, try multiply a scalar.")
+        exponent = PaillierEncoder.cal_exponent(scalar, precision=None)
+        encoded_scalar = PaillierEncoder.encode_single(self.context, scalar, exponent)
+        raw = ops.raw_mul(self.__context, [self.__c], [encoded_scalar])[0]
+        return PaillierCiphertext(self.context, raw, exponent + self.exponent)
+
+    def __rmul__(self, scalar: Union[int, float]):
+        return self.__mul__(scalar)
+
+    def __truediv__(self, scalar: Union[int, float]):
+        return self.__mul__(1 / scalar)
+
+    def obfuscate(self):
+        """paillier.py:189-232 (fresh device-drawn a / r)."""
+        self.__c = ops.obfuscate(self.__context, [self.__c])[0]
+        return self
+
+
+def _to_ciphertexts(context, raws, exps, shape):
+    out = np.empty(len(raws), dtype=object)
+    for i, (r, e) in enumerate(zip(raws, exps)):
+        out[i] = PaillierCiphertext(context, r, int(e))
+    return out.reshape(shape)
+
+
+def _encode_ints(context, xs, precision, max_exponent):
+    """Reference per-element encode for integer elements (encoder.py:29-54)."""
+    ms, es = [], []
+    for x in xs:
+        e = PaillierEncoder.cal_exponent(x, precision)
+        if max_exponent is not None:
+            e = min(e, max_exponent)
+        ms.append(int(PaillierEncoder.encode_single(context, x, e)))
+        es.append(int(e))
+    return ms, es
+
+
+class Paillier(object):
+    """paillier.py:235-431"""
+
+    @staticmethod
+    def context(key_bit_size: int = 2048, djn_on: bool = False):
+        return PaillierContext.generate(key_bit_size, djn_on)
+
+    @staticmethod
+    def context_from(data: bytes):
+        return PaillierContext.deserialize_from(data)
+
+    @staticmethod
+    def serialize(data: Union[np.ndarray, PaillierCiphertext], compression: bool = True) -> bytes:
+        """paillier.py:244-258"""
+        from ..compat import compress, dumps
+        if isinstance(data, PaillierCiphertext):
+            return data.serialize(compression)
+
+        def f(x):
+            return RawCiphertext(x.raw_ciphertext, x.exponent)
+
+        out = dumps(np.vectorize(f)(data))
+        return compress(out) if compression else out
+
+    @staticmethod
+    def ciphertext_from(context: PaillierContext, data: bytes, compression: bool = True):
+        """paillier.py:260-271"""
+        from ..compat import decompress, loads
+        if compression:
+            data = decompress(data)
+        unpickled = loads(data)
+
+        def f(x):
+            return PaillierCiphertext(context, int(x.value), x.exp)
+
+        return np.vectorize(f, otypes=[PaillierCiphertext])(unpickled)
+
+    @classmethod
+    def encrypt(cls, context: PaillierContext, data: Union[int, float, np.ndarray], precision: Optional[int] = None,
+                max_exponent: Optional[int] = None, obfuscation: bool = True,
+                num_cores: int = -1) -> Union[PaillierCiphertext, np.ndarray]:
+        """paillier.py:289-339. num_cores is accepted for compatibility; the
+        elements are spread over GPU lanes instead of processes."""
+        if isinstance(data, np.ndarray):
+            shape = data.shape
+            flat = data.reshape(-1)
+            n = flat.shape[0]
+            raws = [None] * n
+            exps = [0] * n
+            if flat.dtype.kind == "f":
+                r, e, st = ops.encrypt_floats(context, flat.astype(np.float64), precision, max_exponent, obfuscation)
+                Paillier._raise_status(st)
+                raws, exps = r, e
+            else:
+                fl_idx, int_idx = [], []
+                for i, x in enumerate(flat):
+                    if isinstance(x, (float, np.floating)):
+                        fl_idx.append(i)
+                    elif isinstance(x, (int, np.integer)):
+                        int_idx.append(i)
+                    else:
+                        PaillierEncoder.cal_exponent(x, precision)  # raises TypeError like the reference
+                        raise TypeError(f"Unsupported data type {type(x)}")
+                if fl_idx:
+                    r, e, st = ops.encrypt_floats(context, np.array([float(flat[i]) for i in fl_idx]), precision,
+                                                  max_exponent, obfuscation)
+                    Paillier._raise_status(st)
+                    for j, i in enumerate(fl_idx):
+                        raws[i], exps[i] = r[j], int(e[j])
+                if int_idx:
+                    ms, es = _encode_ints(context, [flat[i] for i in int_idx], precision, max_exponent)
+                    r = ops.encrypt_encoded(context, ms, obfuscation)
+                    for j, i in enumerate(int_idx):
+                        raws[i], exps[i] = r[j], es[j]
+            return _to_ciphertexts(context, raws, exps, shape)
+        elif isinstance(data, (int, float)):
+            if isinstance(data, float):
+                r, e, st = ops.encrypt_floats(context, np.array([data]), precision, max_exponent, obfuscation)
+                Paillier._raise_status(st)
+                return PaillierCiphertext(context, r[0], int(e[0]))
+            ms, es = _encode_ints(context, [data], precision, max_exponent)
+            return PaillierCiphertext(context, ops.encrypt_encoded(context, ms, obfuscation)[0], es[0])
+        else:
+            raise TypeError(f"Unsupported data type {type(data)}, accepted types are 'np.ndarray', 'int', 'float'.")
+
+    @staticmethod
+    def _raise_status(st):
+        bad = np.nonzero(st)[0]
+        if bad.size:
+            code = int(st[bad[0]])
+            if code == 2:
+                raise ValueError("cannot convert float NaN to integer / negative shift count")
+            raise OverflowError("cannot convert float infinity to integer / int too large to convert to float")
+
+    @staticmethod
+    def _decrypt_single(data: PaillierCiphertext, context: PaillierContext):
+        """paillier.py:341-368 (non-ciphertexts pass through)."""
+        if not isinstance(data, PaillierCiphertext):
+            return data
+        m = ops.decrypt_ints(context, [data.raw_ciphertext])[0]
+        return PaillierEncoder.decode_single(context, m, data.exponent)
+
+    @classmethod
+    def decrypt(cls, context: PaillierContext, data: Union[PaillierCiphertext, np.ndarray], dtype: str = 'float',
+                num_cores: int = -1, out_origin: bool = False):
+        """paillier.py:370-417"""
+        if not context.is_private():
+            raise TypeError("Try to decrypt a paillier ciphertext by a public key.")
+        if isinstance(data, np.ndarray):
+            shape = data.shape
+            flat = data.reshape(-1)
+            idx = [i for i, x in enumerate(flat) if isinstance(x, PaillierCiphertext)]
+            if not out_origin and dtype == 'float' and len(idx) == len(flat) and len(flat) > 0:
+                _, f32, st = ops.decrypt_float32(context, [x.raw_ciphertext for x in flat],
+                                                 [x.exponent for x in flat])
+                if np.any(st != 0):
+                    raise OverflowError("Overflow detected during decoding encrypted number.")
+                return f32.reshape(shape)
+            vals = list(flat)
+            ms = ops.decrypt_ints(context, [flat[i].raw_ciphertext for i in idx])
+            for i, m in zip(idx, ms):
+                vals[i] = PaillierEncoder.decode_single(context, m, flat[i].exponent)
+            out = np.empty(len(vals), dtype=object)
+            out[:] = vals
+            out = out.reshape(shape)
+            if not out_origin:
+                if dtype == 'float':
+                    out = _astype_f32(out)
+                elif dtype == 'int':
+                    out = out.astype(np.int32)
+                else:
+                    warnings.warn(f"dtype {dtype} not supported.")
+                    out = _astype_f32(out)
+            return out
+        elif isinstance(data, PaillierCiphertext):
+            out = cls._decrypt_single(data, context)
+            if not out_origin:
+                if 'float' in dtype:
+                    out = float(out) if isinstance(out, float) else int_to_float_gmpy(out)
+                elif 'int' in dtype:
+                    out = int(out)
+                else:
+                    warnings.warn(f"dtype {dtype} not supported.")
+                    out = float(out) if isinstance(out, float) else int_to_float_gmpy(out)
+            return out
+        else:
+            raise TypeError(f"Unsupported data type {type(data)}, accepted types are 'np.ndarray', "
+                            "'PaillierCiphertext'.")
+
+    @classmethod
+    def obfuscate(cls, ciphertext: Union[PaillierCiphertext, np.ndarray]):
+        """paillier.py:419-431"""
+        if isinstance(ciphertext, np.ndarray):
+            flat = ciphertext.reshape(-1)
+            if not all(isinstance(c, PaillierCiphertext) for c in flat):
+                raise TypeError("Unsupported raw ciphertext type")
+            if len(flat):
+                ctx = flat[0].context
+                raws = ops.obfuscate(ctx, [c.raw_ciphertext for c in flat])
+                out = np.empty(len(flat), dtype=object)
+                for i, (c, r) in enumerate(zip(flat, raws)):
+                    out[i] = PaillierCiphertext(c.context, r, c.exponent)
+                return out.reshape(ciphertext.shape)
+            return ciphertext
+        elif isinstance(ciphertext, PaillierCiphertext):
+            return ciphertext.obfuscate()
+        else:
+            raise TypeError(f"Unsupported raw ciphertext type {type(ciphertext)}")
+
+
+def _astype_f32(obj_arr):
+    """astype(np.float32) of decode outputs: floats directly, ints through the
+    gmpy2 mpz->float conversion (truncating) like the reference's mpz objects."""
+    flat = obj_arr.reshape(-1)
+    vals = np.empty(len(flat), dtype=np.float64)
+    for i, v in enumerate(flat):
+        if isinstance(v, float):
+            vals[i] = v
+        elif isinstance(v, int):
+            vals[i] = int_to_float_gmpy(v)
+        else:
+            vals[i] = float(v)
+    with np.errstate(over="ignore"):
+        return vals.astype(np.float32).reshape(obj_arr.shape)
