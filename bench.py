@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
     ap.add_argument("--key-bits", type=int, default=2048)
-    ap.add_argument("--win", type=int, default=8)
+    ap.add_argument("--win", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

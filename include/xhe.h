@@ -32,7 +32,9 @@ typedef struct xhe_key xhe_key;
  * (PaillierContext.init, context.py:28-71) and, for a DJN private key, the
  * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win_bits rows per window).
  * p_words/q_words NULL => public key (n only). h_pow_n_words NULL => DJN off.
- * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in {4, 8} (0 = default). */
+ * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in {4, 8, 12, 16};
+ * 0 = default (16, or $XHE_WIN_BITS). A 16-bit window needs 2^16 rows per
+ * window: 2.5 GB of HBM per 2048-bit key (2 x 1.27 GB), built in ~0.1 s. */
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
 void xhe_key_destroy(xhe_key* key);
@@ -82,7 +84,18 @@ int xhe_powmod(const xhe_key* key, const uint32_t* c_dev, const uint32_t* k_dev,
  * (product-tree batch inversion). XHE_ENOINV when some c has no inverse. */
 int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_t* out_dev, void* stream);
 
+/* Homomorphic sum per segment (np.sum / pandas groupby('bin').sum() over
+ * ciphertexts, decision_tree_trainer.py:151-160, xgb_actor.py:340-345,447-456):
+ * out[s] = prod_{i in [seg_begin[s], seg_begin[s+1])} c_i^(2^d_i) mod n^2,
+ * d_i = e_i - (min exponent of the segment) (NULL = all 0), dmax >= max d_i.
+ * seg_begin is a HOST array of nseg+1 offsets into the segment-ordered input;
+ * an empty segment yields 1 (the encryption of 0 without obfuscation). */
+int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev, int dmax, int64_t count,
+                const int64_t* seg_begin, int64_t nseg, uint32_t* out_dev, void* stream);
+
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
+int xhe_segprod_host(const xhe_key* key, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
+                     const int64_t* seg_begin, int64_t nseg, uint32_t* out);
 int xhe_mulmod_host(const xhe_key* key, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
                     int64_t count, int dmax, uint32_t* out, int32_t* eout);
 /* c^k (or (c^-1)^k when invert_first: the negative-scalar branch). */

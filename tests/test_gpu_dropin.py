@@ -33,13 +33,20 @@ def _raw(arr):
         [c.exponent for c in np.asarray(arr, dtype=object).reshape(-1)]
 
 
+@pytest.mark.parametrize("vectorized", [False, True])
 @pytest.mark.parametrize("fx", FIXTURES[:2])
-def test_ops_bit_exact(fx):
+def test_ops_bit_exact(fx, vectorized):
+    """vectorized=False: numpy's per-element object loop over PaillierCiphertext
+    operators; True: PaillierArray's batched kernels (segmented product,
+    batch inversion, multi-exponentiation matmul)."""
+    from xfl_amd.paillier import PaillierArray
     g = load_fixture(fx)
     priv, pub = _ctxs(g)
     ops = g["ops"]
     a = _cts(pub, ops["a"])
     b = _cts(pub, ops["b"])
+    if vectorized:
+        a, b = PaillierArray(a), PaillierArray(b)
     sc = [fl(s) if isinstance(s, str) else s for s in ops["mul_pub"]["scalar"]]
     want = lambda name: ([hx(r) for r in ops[name]["raw"]], ops[name]["exp"])  # noqa: E731
     assert _raw(a + b) == want("add")
@@ -47,6 +54,11 @@ def test_ops_bit_exact(fx):
     assert _raw(np.array([a[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_pub")
     a_priv = _cts(priv, ops["a"])
     assert _raw(np.array([a_priv[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_priv")
+    if vectorized:
+        scv = np.array(sc, dtype=object)
+        assert _raw(a * scv) == want("mul_pub")
+        assert _raw(a + scv) == want("add_scalar")
+        assert _raw(scv - a) == want("rsub_scalar")
     assert _raw(np.array([a[i] + sc[i] for i in range(len(a))], dtype=object)) == want("add_scalar")
     assert _raw(np.array([sc[i] - a[i] for i in range(len(a))], dtype=object)) == want("rsub_scalar")
     assert _raw(a / 4.0) == want("truediv")

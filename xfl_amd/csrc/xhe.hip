@@ -1,6 +1,7 @@
 // xhe: C-ABI over the gfx950 Paillier kernels (see include/xhe.h).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <cmath>
@@ -134,7 +135,11 @@ void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t
   HIPCHK(hipGetLastError());
   int groups_per_block = 64 / MP2::TPI;
   int blocks = (k->kd.nwin + groups_per_block - 1) / groups_per_block;
-  hipLaunchKernelGGL(k_tab_fill<MP2>, dim3(blocks), dim3(64), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
+  hipLaunchKernelGGL(k_tab_chain<MP2>, dim3(blocks), dim3(64), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
+  HIPCHK(hipGetLastError());
+  int64_t rows = (int64_t)k->kd.nwin << k->kd.win;
+  int cblocks = (int)((rows * MP2::TPI + 255) / 256);
+  hipLaunchKernelGGL(k_tab_combine<MP2>, dim3(cblocks), dim3(256), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipFree(d_ws));
@@ -528,6 +533,63 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   return XHE_OK;
 }
 
+// Segmented modular product: out[s] = prod_{i in seg s} c_i^(2^d_i) mod n^2.
+// seg_begin: nseg+1 offsets into the (already segment-ordered) inputs.
+template <class Sh>
+void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
+                  const int64_t* seg_begin_host, int64_t nseg, uint32_t* out, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  const int S4 = MN2::S4;
+  const int64_t C = 32;  // chunk length per level
+  auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
+  uint32_t *rows = nullptr, *sq = nullptr;
+  HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+  HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+  if (count > 0) {
+    hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, d, count, dmax,
+                       rows, sq);
+    HIPCHK(hipGetLastError());
+  }
+  std::vector<int64_t> seg(seg_begin_host, seg_begin_host + nseg + 1);
+  int64_t n_cur = count;
+  uint32_t* cur = rows;
+  std::vector<uint32_t*> to_free{sq};
+  while (true) {
+    bool done = true;
+    for (int64_t i = 0; i < nseg; ++i)
+      if (seg[i + 1] - seg[i] != 1) { done = false; break; }
+    // chunk boundaries: each segment split into ceil(len/C) chunks (>= 1 chunk)
+    std::vector<int64_t> cb{0}, nseg_b{0};
+    for (int64_t i = 0; i < nseg; ++i) {
+      int64_t len = seg[i + 1] - seg[i];
+      int64_t nch = done ? 1 : std::max<int64_t>(1, (len + C - 1) / C);
+      for (int64_t t = 0; t < nch; ++t) cb.push_back(std::min(seg[i + 1], seg[i] + (t + 1) * (done ? len : C)));
+      nseg_b.push_back(nseg_b.back() + nch);
+    }
+    int64_t n_out = (int64_t)cb.size() - 1;
+    int64_t* dcb = nullptr;
+    uint32_t* nxt = nullptr;
+    HIPCHK(hipMallocAsync((void**)&dcb, cb.size() * 8, s));
+    HIPCHK(hipMemcpyAsync(dcb, cb.data(), cb.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(n_out, 1) * 4, s));
+    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, k->kd.n2.N, cur, n_cur, dcb, n_out,
+                       nxt);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // cb lives on the host stack
+    (void)hipFree(dcb);
+    (void)hipFree(cur);
+    cur = nxt;
+    n_cur = n_out;
+    seg = nseg_b;
+    if (done) break;
+  }
+  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, k->kd.n2.N, cur, nseg, out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(cur);
+  for (auto p : to_free) (void)hipFree(p);
+}
+
 template <class Sh>
 void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32_t* ct, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -587,6 +649,21 @@ int guarded(F&& f) {
 
 }  // namespace
 
+int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev, int dmax, int64_t count,
+                const int64_t* seg_begin, int64_t nseg, uint32_t* out_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || !seg_begin || nseg <= 0 || (count > 0 && !c_dev) || !out_dev || dmax < 0)
+      return fail(XHE_EINVAL, "xhe_segprod: bad argument");
+    if (seg_begin[0] != 0 || seg_begin[nseg] != count) return fail(XHE_EINVAL, "xhe_segprod: bad segment offsets");
+    for (int64_t i = 0; i < nseg; ++i)
+      if (seg_begin[i + 1] < seg_begin[i]) return fail(XHE_EINVAL, "xhe_segprod: offsets must be non-decreasing");
+    DevGuard dg(key->device);
+    if (key->K == 2048) segprod_impl<Shape2048>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, (hipStream_t)stream);
+    else segprod_impl<Shape3072>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
 namespace {
 struct DevBuf {
   void* p = nullptr;
@@ -615,8 +692,12 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     if (key_bits != 2048 && key_bits != 3072)
       return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048 or 3072");
     if ((p_words == nullptr) != (q_words == nullptr)) return fail(XHE_EINVAL, "xhe_key_create: need both p and q");
-    if (win_bits == 0) win_bits = 8;
-    if (win_bits != 4 && win_bits != 8) return fail(XHE_EINVAL, "xhe_key_create: win_bits must be 4 or 8");
+    if (win_bits == 0) {
+      const char* ev = getenv("XHE_WIN_BITS");
+      win_bits = ev ? atoi(ev) : 16;
+    }
+    if (win_bits != 4 && win_bits != 8 && win_bits != 12 && win_bits != 16)
+      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be 4, 8, 12 or 16");
     std::unique_ptr<xhe_key> k(new xhe_key());
     k->device = device;
     k->K = key_bits;
@@ -967,6 +1048,25 @@ int xhe_powmod_host(const xhe_key* key, const uint32_t* c, const uint32_t* k, in
     int rc = xhe_powmod(key, base, dk.as<uint32_t>(), kw, kbits, count, dout.as<uint32_t>(), st.s);
     if (rc != XHE_OK) return rc;
     HIPCHK(hipMemcpyAsync(out, dout.p, cw, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_segprod_host(const xhe_key* key, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
+                     const int64_t* seg_begin, int64_t nseg, uint32_t* out) {
+  return guarded([&]() -> int {
+    if (!key || !seg_begin || nseg <= 0 || (count > 0 && !c) || !out) return fail(XHE_EINVAL, "xhe_segprod_host: bad argument");
+    DevGuard dg(key->device);
+    Stream st;
+    size_t cw = (size_t)std::max<int64_t>(count, 1) * key->n2w * 4;
+    DevBuf dc(cw, st.s), dd((size_t)std::max<int64_t>(count, 1) * 4, st.s), dout((size_t)nseg * key->n2w * 4, st.s);
+    if (count > 0) HIPCHK(hipMemcpyAsync(dc.p, c, (size_t)count * key->n2w * 4, hipMemcpyHostToDevice, st.s));
+    if (d && count > 0) HIPCHK(hipMemcpyAsync(dd.p, d, count * 4, hipMemcpyHostToDevice, st.s));
+    int rc = xhe_segprod(key, dc.as<uint32_t>(), d ? dd.as<int32_t>() : nullptr, dmax, count, seg_begin, nseg,
+                         dout.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(out, dout.p, (size_t)nseg * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
     HIPCHK(hipStreamSynchronize(st.s));
     return XHE_OK;
   });

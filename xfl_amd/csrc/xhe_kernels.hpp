@@ -206,13 +206,21 @@ __global__ void k_rand_below(ChaChaKey ck, int64_t count, int words, int bits, c
 }
 
 // ============================================================== encrypt
+// win-bit digit starting at bit `bit` of a little-endian word array (may
+// straddle two words; bits beyond nwords read as zero)
+XHE_DEV uint32_t digit_at(const uint32_t* w, int nwords, int bit, int win) {
+  int k = bit >> 5, sh = bit & 31;
+  uint64_t v = (uint64_t)(k < nwords ? w[k] : 0u) | ((uint64_t)(k + 1 < nwords ? w[k + 1] : 0u) << 32);
+  return (uint32_t)(v >> sh) & ((1u << win) - 1u);
+}
+
 template <class MP2>
 XHE_DEV void fixed_base_pow(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* tab, int win, int nwin,
                             const uint32_t* __restrict__ a_words) {
   const int rows = 1 << win;
   for (int w = 0; w < nwin; ++w) {
     int bit = w * win;
-    uint32_t d = (a_words[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    uint32_t d = digit_at(a_words, nwin * win / 32 + 1, bit, win);
     M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
   }
 }
@@ -246,7 +254,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
     int bit = w * key.win;
-    uint32_t d = (ae[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    uint32_t d = digit_at(ae, aw, bit, key.win);
     M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
   }
   M.mul(b, AOne{});
@@ -579,7 +587,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* 
   const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
     int bit = w * key.win;
-    uint32_t d = (ae[bit >> 5] >> (bit & 31)) & (uint32_t)(rows - 1);
+    uint32_t d = digit_at(ae, aw, bit, key.win);
     M.mul(b, ARow{key.tab_n2 + ((size_t)w * rows + d) * MN2::S4});
   }
   M.mul(b, AOne{});
@@ -653,6 +661,57 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t
                prime ? key.eq_bits : key.ep_bits, tab, tab + 16 * rs, tab + 17 * rs, st);
     M.store_strided(b, rows + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
   }
+}
+
+// ---- homomorphic sums / histograms (A.9, decision_tree_trainer.py:151-160)
+// Each element enters as c^(2^d) R (Montgomery), d = e - e_min of its segment.
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_align_mont(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                       const uint32_t* __restrict__ c, const int32_t* __restrict__ d,
+                                                       int64_t count, int dmax, uint32_t* __restrict__ rows,
+                                                       uint32_t* __restrict__ sqws) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (e >= count) return;
+  const int st = (int)count;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
+  M.mul(b, ARow{key.n2.R2});
+  const int de = d ? d[e] : 0;
+  for (int k = 0; k < dmax; ++k) {
+    if (k < de) {
+      M.store_strided(b, sqws + e, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sqws + e, st});
+    }
+  }
+  M.reduce_once(b);
+  M.store_strided(b, rows + e, st);
+}
+
+// One reduction level: chunk j multiplies rows [cbeg[j], cbeg[j+1]) (Montgomery
+// rows [S4][n_in]) into out row j ([S4][n_out]).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_chunk_prod(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                       const uint32_t* __restrict__ in, int64_t n_in,
+                                                       const int64_t* __restrict__ cbeg, int64_t n_out,
+                                                       uint32_t* __restrict__ outp) {
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (j >= n_out) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  const int64_t lo = cbeg[j], hi = cbeg[j + 1];
+  if (hi <= lo) {  // empty segment: Montgomery one
+    M.load_row(b, key.n2.R1);
+    M.reduce_once(b);
+  } else {
+    M.load_strided(b, in + lo, (int)n_in);
+    for (int64_t i = lo + 1; i < hi; ++i) M.mul(b, AStrided{in + i, (int)n_in});
+    M.reduce_once(b);
+  }
+  M.store_strided(b, outp + j, (int)n_out);
 }
 
 // ---- batch modular inversion mod n^2 (Montgomery's trick as a product tree)
@@ -847,25 +906,59 @@ __global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* 
   }
 }
 
-// k_tab_fill: one group per window w: tab[w][0] = R, tab[w][d] = tab[w][d-1] * tab[w][1]
+// k_tab_chain: one group per window w, half = win/2. With B = tab[w][1]:
+//   tab[w][d]          = B^d            for d < 2^half          (low chain)
+//   tab[w][d << half]  = B^(d << half)  for 0 < d < 2^half      (high chain)
+// k_tab_combine then fills tab[w][hi|lo] = tab[w][hi] * tab[w][lo].
 template <class MP2>
-__global__ void __launch_bounds__(64, 2) k_tab_fill(ModDev md, int win, int nwin, uint32_t* tab) {
+__global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, int win, int nwin, uint32_t* tab) {
   const int w = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI);
   if (w >= nwin) return;
   MP2 M;
   M.init(md.N, md.n0inv);
-  const int rows = 1 << win;
-  uint32_t* t = tab + (size_t)w * rows * MP2::S4;
+  const int half = win / 2, lo_n = 1 << half;
+  uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
   uint32_t b[MP2::L];
   M.load_row(b, md.R1);
   M.reduce_once(b);
-  M.store_row(b, t);
+  M.store_row(b, t);  // B^0 = R
   M.load_row(b, t + MP2::S4);
-  for (int d = 2; d < rows; ++d) {
+  for (int d = 2; d < lo_n; ++d) {
     M.mul(b, ARow{t + MP2::S4});
     M.reduce_once(b);
     M.store_row(b, t + (size_t)d * MP2::S4);
   }
+  // G = B^(2^half) = B^(2^half - 1) * B
+  M.mul(b, ARow{t + MP2::S4});
+  M.reduce_once(b);
+  const size_t gs = (size_t)lo_n * MP2::S4;  // row stride of the high chain
+  M.store_row(b, t + gs);
+  wave_sync_mem_();
+  for (int d = 2; d < lo_n; ++d) {
+    M.mul(b, ARow{t + gs});
+    M.reduce_once(b);
+    M.store_row(b, t + (size_t)d * gs);
+  }
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, int win, int nwin, uint32_t* tab) {
+  const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  const int64_t rows = (int64_t)nwin << win;
+  if (idx >= rows) return;
+  const int half = win / 2;
+  const int w = (int)(idx >> win);
+  const int d = (int)(idx & ((1 << win) - 1));
+  const int lo = d & ((1 << half) - 1), hi = d >> half;
+  if (lo == 0 || hi == 0) return;  // chain entries
+  uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
+  MP2 M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_row(b, t + ((size_t)hi << half) * MP2::S4);
+  M.mul(b, ARow{t + (size_t)lo * MP2::S4});
+  M.reduce_once(b);
+  M.store_row(b, t + (size_t)d * MP2::S4);
 }
 
 // Montgomery product of two rows (host-side setup helper / unit tests):

@@ -2,3 +2,4 @@
 from .context import PaillierContext  # noqa: F401
 from .encoder import PaillierEncoder  # noqa: F401
 from .paillier import Paillier, PaillierCiphertext, RawCiphertext  # noqa: F401
+from .array import PaillierArray  # noqa: F401

@@ -149,3 +149,26 @@ def obfuscate(ctx, raws):
     z = np.zeros(n, dtype=np.int32)
     r, _ = add(ctx, raws, z, xs, z)
     return r
+
+
+def segment_sums(ctx, raws, exps, seg_begin):
+    """Homomorphic sums of consecutive segments: segment s covers
+    [seg_begin[s], seg_begin[s+1]); result exponent = min exponent of the
+    segment (paillier.py:106-123 folded; order-free)."""
+    dk = ctx.device_key()
+    seg = np.ascontiguousarray(seg_begin, dtype=np.int64)
+    nseg = seg.shape[0] - 1
+    n = len(raws)
+    e = np.asarray(exps, dtype=np.int64)
+    emin = np.zeros(nseg, dtype=np.int64)
+    d = np.zeros(n, dtype=np.int32)
+    for s in range(nseg):
+        lo, hi = int(seg[s]), int(seg[s + 1])
+        if hi > lo:
+            emin[s] = e[lo:hi].min()
+            d[lo:hi] = (e[lo:hi] - emin[s]).astype(np.int32)
+    dmax = int(d.max()) if n else 0
+    cw = nat.ints_to_words(raws, dk.n2w) if n else np.zeros((1, dk.n2w), dtype=np.uint32)
+    out = np.empty((nseg, dk.n2w), dtype=np.uint32)
+    nat.check(nat.lib().xhe_segprod_host(dk.handle, _vp(cw), _vp(d), dmax, n, _vp(seg), nseg, _vp(out)), "segprod")
+    return nat.words_to_ints(out), emin

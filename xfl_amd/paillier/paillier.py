@@ -121,10 +121,11 @@ class PaillierCiphertext(object):
 
 
 def _to_ciphertexts(context, raws, exps, shape):
+    from .array import PaillierArray
     out = np.empty(len(raws), dtype=object)
     for i, (r, e) in enumerate(zip(raws, exps)):
         out[i] = PaillierCiphertext(context, r, int(e))
-    return out.reshape(shape)
+    return out.reshape(shape).view(PaillierArray)
 
 
 def _encode_ints(context, xs, precision, max_exponent):
@@ -174,7 +175,8 @@ class Paillier(object):
         def f(x):
             return PaillierCiphertext(context, int(x.value), x.exp)
 
-        return np.vectorize(f, otypes=[PaillierCiphertext])(unpickled)
+        from .array import PaillierArray
+        return np.vectorize(f, otypes=[PaillierCiphertext])(unpickled).view(PaillierArray)
 
     @classmethod
     def encrypt(cls, context: PaillierContext, data: Union[int, float, np.ndarray], precision: Optional[int] = None,
@@ -301,7 +303,8 @@ class Paillier(object):
                 out = np.empty(len(flat), dtype=object)
                 for i, (c, r) in enumerate(zip(flat, raws)):
                     out[i] = PaillierCiphertext(c.context, r, c.exponent)
-                return out.reshape(ciphertext.shape)
+                from .array import PaillierArray
+                return out.reshape(ciphertext.shape).view(PaillierArray)
             return ciphertext
         elif isinstance(ciphertext, PaillierCiphertext):
             return ciphertext.obfuscate()
