@@ -56,10 +56,22 @@ def algorithmic_macs_per_element(bits, win, rand_bits):
 
 
 def cpu_baseline(bits, seconds, cores):
-    """Reference-algorithm port (oracle/paillier_oracle.py, pure-Python pow,
-    the GMP-free restatement) timed on this host for a bounded sample."""
+    """The reference algorithm timed on this host for a bounded sample:
+    preferably the C port on GMP's mpz_powm (what gmpy2 calls; oracle/
+    gmp_baseline.c, dlopen libgmp.so.10) over `cores` threads, else the
+    pure-Python restatement (oracle/paillier_oracle.py) over `cores` processes."""
     import multiprocessing as mp
     from oracle import bench_cpu
+    try:
+        r = bench_cpu.gmp_rate(bits, seconds, cores)
+    except Exception:
+        r = None
+    if r is not None:
+        total, wall = r
+        return {"value": total / wall, "unit": "encrypts/s", "cores": cores, "kind": "port",
+                "sample": f"{total} DJN-CRT private-key encryptions (2 mpz_powm mod p^2/q^2 + CRT + mulmod, "
+                          f"precision-7 encode), {cores} threads x ~{seconds:.0f}s, C port on system GMP "
+                          "(oracle/gmp_baseline.c) - same GMP routines as the reference's gmpy2"}
     with mp.get_context("fork").Pool(cores) as pool:
         t0 = time.time()
         counts = pool.map(bench_cpu.encrypt_for, [(bits, seconds, i) for i in range(cores)])

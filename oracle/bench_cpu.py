@@ -34,3 +34,61 @@ def encrypt_for(arg):
         O.encrypt_m(k, m, rng.randrange(1, bound))
         count += 1
     return count
+
+
+# ---------------------------------------------------------------- GMP port
+def _gmp_lib():
+    import ctypes
+    from oracle import build
+    path = build.build()
+    if path is None:
+        return None
+    L = ctypes.CDLL(path)
+    if L.gmpb_load() != 0:
+        return None
+    return L
+
+
+def _key_words(k, nw):
+    import numpy as np
+
+    def w(x, n):
+        return np.frombuffer(int(x).to_bytes(4 * n, "little"), dtype="<u4").copy()
+
+    return [w(k["n"], nw), w(k["n_square"], 2 * nw), w(k["p_square"], nw), w(k["q_square"], nw),
+            w(k["q2_inverse_p2"], nw), w(k["h_pow_n_modp2"], nw), w(k["h_pow_n_modq2"], nw)]
+
+
+def gmp_encrypt_one(k, m, a):
+    """One DJN-CRT encryption through the GMP port (for checking it)."""
+    import ctypes
+    import numpy as np
+    L = _gmp_lib()
+    nw = (k["n"].bit_length() + 31) // 32
+    arrs = _key_words(k, nw)
+    aw = np.frombuffer(int(a).to_bytes(128, "little"), dtype="<u4").copy()
+    out = np.zeros(2 * nw, dtype=np.uint32)
+    args = [x.ctypes.data_as(ctypes.c_void_p) for x in arrs]
+    rc = L.gmpb_encrypt_one(*args, ctypes.c_int(nw), ctypes.c_longlong(m), aw.ctypes.data_as(ctypes.c_void_p),
+                            ctypes.c_int(32), out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return int.from_bytes(out.tobytes(), "little")
+
+
+def gmp_rate(bits, seconds, threads):
+    """(encryptions, wall seconds) of the GMP port over `threads` threads, or None."""
+    import ctypes
+    L = _gmp_lib()
+    if L is None:
+        return None
+    k = _key(bits)
+    nw = bits // 32
+    arrs = _key_words(k, nw)
+    args = [x.ctypes.data_as(ctypes.c_void_p) for x in arrs]
+    tot = ctypes.c_uint64()
+    wall = ctypes.c_double()
+    rc = L.gmpb_bench(*args, ctypes.c_int(nw), ctypes.c_double(seconds), ctypes.c_int(threads), ctypes.byref(tot),
+                      ctypes.byref(wall))
+    if rc != 0:
+        return None
+    return tot.value, wall.value
