@@ -82,6 +82,81 @@ def cpu_baseline(bits, seconds, cores):
                       f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
 
 
+def _timed(fn, reps=3):
+    """Average seconds per call of fn() on the current stream (1 untimed warm call)."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.time() - t0) / reps
+
+
+def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream):
+    """Rates of the other operations on the path (BASELINE configs 2, 3, 5),
+    device-resident except where named; plus the host-buffer (PCIe-inclusive)
+    encrypt/decrypt rates. Each is checked where a cheap property exists."""
+    import ctypes
+    import torch
+    out = {}
+    # config 2: decrypt the step's ciphertexts; round trip must give back m exactly
+    m2 = torch.empty_like(m)
+    t = _timed(lambda: nat.check(L.xhe_decrypt(dk.handle, ct.data_ptr(), N, m2.data_ptr(), stream), "decrypt"))
+    out["decrypt_per_s"] = N / t
+    out["roundtrip_bit_exact"] = bool(torch.equal(m, m2))
+    # ciphertext add (paillier.py:153-154), equal exponents
+    ct2 = torch.empty_like(ct)
+    t = _timed(lambda: nat.check(L.xhe_mulmod(dk.handle, ct.data_ptr(), None, ct.data_ptr(), None, N, 0,
+                                              ct2.data_ptr(), None, stream), "add"))
+    out["add_per_s"] = N / t
+    # add with exponent alignment: operands one exponent apart (x * 2^-1 precision shift)
+    e1 = torch.zeros(N, dtype=torch.int32, device="cuda")
+    e2 = torch.full((N,), -4, dtype=torch.int32, device="cuda")
+    t = _timed(lambda: nat.check(L.xhe_mulmod(dk.handle, ct.data_ptr(), e1.data_ptr(), ct.data_ptr(), e2.data_ptr(),
+                                              N, 4, ct2.data_ptr(), None, stream), "add_align"))
+    out["add_aligned_d4_per_s"] = N / t
+    # scalar mul by an encoded float64 (53-bit mantissa, positive branch, paillier.py:156-187)
+    nk = min(N, 1 << 18)
+    k = torch.randint(0, 1 << 31, (nk, 2), dtype=torch.int64, device="cuda").to(torch.int32)
+    k[:, 1] &= (1 << 21) - 1
+    k[:, 1] |= 1 << 20
+    t = _timed(lambda: nat.check(L.xhe_powmod(dk.handle, ct.data_ptr(), k.data_ptr(), 2, 53, nk, ct2.data_ptr(),
+                                              stream), "scalar_mul"))
+    out["scalar_mul_53bit_per_s"] = nk / t
+    # config 5: 256-bin histogram of 100k ciphertexts (grad) -> segment products
+    ns, nb = min(N, 100_000), 256
+    seg = (np.arange(nb + 1, dtype=np.int64) * ns) // nb
+    hist = torch.empty((nb, dk.n2w), dtype=torch.int32, device="cuda")
+    segp = seg.ctypes.data_as(ctypes.c_void_p)
+    t = _timed(lambda: nat.check(L.xhe_segprod(dk.handle, ct.data_ptr(), None, 0, ns, segp, nb, hist.data_ptr(),
+                                               stream), "hist"))
+    out["hist_256x100k_s"] = t
+    # sum of the whole vector (config 3's aggregation)
+    one = np.array([0, N], dtype=np.int64)
+    t = _timed(lambda: nat.check(L.xhe_segprod(dk.handle, ct.data_ptr(), None, 0, N, one.ctypes.data_as(
+        ctypes.c_void_p), 1, hist.data_ptr(), stream), "sum"), reps=2)
+    out["sum_per_s"] = N / t
+    # host buffers in and out (PCIe-inclusive), the rate the federated exchange sees
+    nh = min(N, 1 << 18)
+    xh = x[:nh].cpu().numpy()
+    cth = np.empty((nh, dk.n2w), dtype=np.uint32)
+    exh = np.empty(nh, dtype=np.int32)
+    sth = np.empty(nh, dtype=np.int32)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    t = _timed(lambda: nat.check(L.xhe_encrypt_f64_host(dk.handle, vp(xh), nh, 7, 0, 0, 1, os.urandom(32), 7,
+                                                        vp(cth), vp(exh), vp(sth)), "encrypt_host"), reps=2)
+    out["encrypt_host_buffers_per_s"] = nh / t
+    f64 = np.empty(nh, dtype=np.float64)
+    f32 = np.empty(nh, dtype=np.float32)
+    t = _timed(lambda: nat.check(L.xhe_decrypt_decode_host(dk.handle, vp(cth), vp(exh), nh, vp(f64), vp(f32), vp(sth),
+                                                           None), "decrypt_host"), reps=2)
+    out["decrypt_decode_host_buffers_per_s"] = nh / t
+    out["host_roundtrip_max_abs_err"] = float(np.max(np.abs(f64 - xh)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,9 +164,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
     ap.add_argument("--key-bits", type=int, default=2048)
-    ap.add_argument("--win", type=int, default=16)
+    ap.add_argument("--win", type=int, default=20, help="fixed-base window bits (20: 2 x 16 GB tables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
     args = ap.parse_args()
 
     import torch
@@ -196,6 +272,8 @@ def main():
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,
         }
+        if not args.no_ops:
+            rec["ops"] = measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream)
         if not args.no_cpu_baseline:
             cores = min(os.cpu_count() or 1, 16)
             rec["cpu_baseline"] = cpu_baseline(bits, args.cpu_seconds, cores)

@@ -32,9 +32,10 @@ typedef struct xhe_key xhe_key;
  * (PaillierContext.init, context.py:28-71) and, for a DJN private key, the
  * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win_bits rows per window).
  * p_words/q_words NULL => public key (n only). h_pow_n_words NULL => DJN off.
- * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in {4, 8, 12, 16};
- * 0 = default (16, or $XHE_WIN_BITS). A 16-bit window needs 2^16 rows per
- * window: 2.5 GB of HBM per 2048-bit key (2 x 1.27 GB), built in ~0.1 s. */
+ * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in [2, 22];
+ * 0 = default (16, or $XHE_WIN_BITS). Tables take ceil(rand_bits/win) x
+ * 2^win rows of S4 words per prime: 2048-bit key, win 16: 2 x 1.27 GB;
+ * win 20: 2 x 16.1 GB (52 instead of 64 products per prime). */
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
 void xhe_key_destroy(xhe_key* key);

@@ -89,11 +89,32 @@ struct ARow {  // one contiguous row of W-limbs (16-byte aligned)
   const uint32_t* __restrict__ p;
   XHE_DEV uint4 load4(int i) const { return *reinterpret_cast<const uint4*>(p + i); }
 };
+// Launder a per-lane pointer: the address arithmetic that follows cannot be
+// hoisted above this point. Without it LICM precomputes the 64-bit address of
+// every limb of an interleaved row (2 VGPRs per limb) outside the loops and
+// the Montgomery state spills.
+// The zero offset goes through the asm (not the pointer) so the compiler keeps
+// the global address space of p (a laundered pointer becomes flat_* accesses).
+XHE_DEV const uint32_t* opaque(const uint32_t* p) {
+  int zero = 0;
+  asm volatile("" : "+s"(zero));
+  return p + zero;
+}
+XHE_DEV uint32_t* opaque(uint32_t* p) {
+  int zero = 0;
+  asm volatile("" : "+s"(zero));
+  return p + zero;
+}
+XHE_DEV int opaque_i(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 struct AStrided {  // interleaved workspace row: limb i at p[i*stride]
   const uint32_t* p;
   int stride;
   XHE_DEV uint4 load4(int i) const {
-    const uint32_t* q = p + (size_t)i * stride;
+    const uint32_t* q = opaque(p) + (size_t)i * stride;
     return make_uint4(q[0], q[stride], q[2 * (size_t)stride], q[3 * (size_t)stride]);
   }
 };
@@ -418,24 +439,42 @@ struct Mont {
 
   // ---------------------------------------------------------------- I/O
   // Load W-limbs from a little-endian 32-bit word array of nwords words.
-  XHE_DEV void load_words(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
-    const int g = G::g();
+  // Limbs of a packed little-endian word array (zero beyond nwords). The lane
+  // index is dispatched to compile-time copies so every word is loaded once
+  // and every shift is an immediate (a runtime lane offset made the compiler
+  // keep 2 loads + a 64-bit address per limb live and spill).
+  template <int GG>
+  XHE_DEV void load_words_g(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-      int bit = W * (g * L + j);
-      int k = bit >> 5, sh = bit & 31;
+      const int bit = W * (GG * L + j);
+      const int k = bit >> 5, sh = bit & 31;
       uint32_t lo = k < nwords ? w[k] : 0u;
-      uint32_t hi = k + 1 < nwords ? w[k + 1] : 0u;
+      uint32_t hi = (sh + W > 32 && k + 1 < nwords) ? w[k + 1] : 0u;
       b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
+    }
+  }
+  XHE_DEV void load_words(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
+    if constexpr (TPI == 1) {
+      load_words_g<0>(b, w, nwords);
+    } else {
+      switch (G::g()) {
+        case 0: load_words_g<0>(b, w, nwords); break;
+        case 1: load_words_g<1>(b, w, nwords); break;
+        case 2: if constexpr (TPI > 2) load_words_g<2>(b, w, nwords); break;
+        default: if constexpr (TPI > 2) load_words_g<TPI - 1>(b, w, nwords); break;
+      }
     }
   }
   // Store this lane's limbs one per word into an interleaved row.
   XHE_DEV void store_strided(const uint32_t (&b)[L], uint32_t* p, int stride) const {
+    p = opaque(p);
     const int g = G::g();
 #pragma unroll
     for (int j = 0; j < L; ++j) p[(size_t)(g * L + j) * stride] = b[j];
   }
   XHE_DEV void load_strided(uint32_t (&b)[L], const uint32_t* p, int stride) const {
+    p = opaque(p);
     const int g = G::g();
 #pragma unroll
     for (int j = 0; j < L; ++j) b[j] = p[(size_t)(g * L + j) * stride];

@@ -135,11 +135,11 @@ void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t
   HIPCHK(hipGetLastError());
   int groups_per_block = 64 / MP2::TPI;
   int blocks = (k->kd.nwin + groups_per_block - 1) / groups_per_block;
-  hipLaunchKernelGGL(k_tab_chain<MP2>, dim3(blocks), dim3(64), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
+  hipLaunchKernelGGL(k_tab_chain<MP2>, dim3(blocks), dim3(64), 0, s, md, md.N, k->kd.win, k->kd.nwin, d_tab);
   HIPCHK(hipGetLastError());
   int64_t rows = (int64_t)k->kd.nwin << k->kd.win;
   int cblocks = (int)((rows * MP2::TPI + 255) / 256);
-  hipLaunchKernelGGL(k_tab_combine<MP2>, dim3(cblocks), dim3(256), 0, s, md, k->kd.win, k->kd.nwin, d_tab);
+  hipLaunchKernelGGL(k_tab_combine<MP2>, dim3(cblocks), dim3(256), 0, s, md, md.N, k->kd.win, k->kd.nwin, d_tab);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipFree(d_ws));
@@ -371,7 +371,8 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
                          r + (size_t)off * k->rand_words, k->rand_words, n, ws);
       HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, n, ws, ct + (size_t)off * k->n2w);
+    hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws,
+                       ct + (size_t)off * k->n2w);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipFreeAsync(ws, s));
@@ -421,7 +422,8 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
         HIPCHK(hipGetLastError());
       }
       int blocks = (int)((n * MP2::TPI + 255) / 256);
-      hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, n, rows, ct + (size_t)off * k->n2w);
+      hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, rows,
+                         ct + (size_t)off * k->n2w);
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipFreeAsync(ws, s));
@@ -621,14 +623,16 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
     int64_t n = std::min(chunk, count - off);
     {
       ProfScope ps("k_dec_pow", s);
-      hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, ct + (size_t)off * k->n2w, n,
-                         xrows, ws);
+      hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
+                         ct + (size_t)off * k->n2w, n, xrows, ws);
       HIPCHK(hipGetLastError());
     }
     int blocks = (int)((n * MP::TPI + 255) / 256);
-    hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, n, xrows, mrows);
+    hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p.N, k->kd.q.N, n,
+                       xrows, mrows);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_crt_dec<MP>, dim3(blocks), dim3(256), 0, s, k->kd, n, mrows, m + (size_t)off * k->nw);
+    hipLaunchKernelGGL(k_crt_dec<MP>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p.N, n, mrows,
+                       m + (size_t)off * k->nw);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipFreeAsync(ws, s));
@@ -696,8 +700,8 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
       const char* ev = getenv("XHE_WIN_BITS");
       win_bits = ev ? atoi(ev) : 16;
     }
-    if (win_bits != 4 && win_bits != 8 && win_bits != 12 && win_bits != 16)
-      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be 4, 8, 12 or 16");
+    if (win_bits < 2 || win_bits > 22)
+      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be in [2, 22]");
     std::unique_ptr<xhe_key> k(new xhe_key());
     k->device = device;
     k->K = key_bits;

@@ -263,15 +263,15 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
 }
 
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, int64_t count, uint32_t* __restrict__ ws,
-                                                    uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
+                                                    uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   if (e >= count) return;
   uint32_t* rp = ws + e;
   uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + e;
   const int st = (int)count;
   MP2 M;
-  M.init(key.p2.N, key.p2.n0inv);
+  M.init(Np2, key.p2.n0inv);
   uint32_t b[MP2::L];
   M.load_strided(b, rp, st);
   M.add_sub_rows(b, key.p2x4_lim, rq, st);
@@ -313,6 +313,7 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
   M.store_strided(b, tab + rs, st);         // tab[1] = b
   wave_sync_mem_();
+#pragma unroll 1
   for (int t = 2; t < 16; ++t) {
     M.mul(b, AStrided{tab + rs, st});  // tab[t] = tab[t-1] * tab[1]
     M.store_strided(b, tab + rs * t, st);
@@ -335,7 +336,9 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
 }
 
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* __restrict__ c_words, int64_t count,
+__global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* __restrict__ Np2,
+                                                    const uint32_t* __restrict__ Nq2,
+                                                    const uint32_t* __restrict__ c_words, int64_t count,
                                                     uint32_t* __restrict__ xrows, uint32_t* __restrict__ ws) {
   const int prime = blockIdx.y;
   const ModDev& md = prime ? key.q2 : key.p2;
@@ -351,7 +354,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
   for (int64_t e = gid0; e < count; e += G_total) {
     const uint32_t* cw = c_words + (size_t)e * n2w;
     MP2 M;
-    M.init(md.N, md.n0inv);
+    M.init(prime ? Nq2 : Np2, md.n0inv);
     uint32_t b[MP2::L];
     // high limbs [S, 2S) of c into the sq row, then REDC(c) * R^3 = c R mod P^2
     {
@@ -385,8 +388,9 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
 // k_dec_fin: m_P = (X_P * P^-1 mod 2^(W*S1)) * hP mod P  (exact division: L_P,
 // context.py:190-194), written to mrows [prime][2*S4][count] (MP limbs).
 template <class MP2, class MP>
-__global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, int64_t count, const uint32_t* __restrict__ xrows,
-                                                    uint32_t* __restrict__ mrows) {
+__global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, const uint32_t* __restrict__ Np,
+                                                    const uint32_t* __restrict__ Nq, int64_t count,
+                                                    const uint32_t* __restrict__ xrows, uint32_t* __restrict__ mrows) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP::TPI;
   if (e >= count) return;
   const int prime = blockIdx.y;
@@ -395,7 +399,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, int64_t count, c
   const int st = (int)count;
   uint32_t* mrow = mrows + (size_t)prime * 2 * MP::S4 * count + e;
   MP M;
-  M.init(md.N, md.n0inv);
+  M.init(prime ? Nq : Np, md.n0inv);
   uint32_t q[MP::L];
   M.load_strided(q, xrows + (size_t)prime * MP2::S4 * count + e, st);  // low S1 limbs of X
   {
@@ -429,15 +433,15 @@ __global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, int64_t count, c
 
 // k_crt_dec: u = (mp + 2p - mq) q^-1 mod p ; m = mq + u q   (utils.py:38-43)
 template <class MP>
-__global__ void __launch_bounds__(256, 2) k_crt_dec(KeyDev key, int64_t count, uint32_t* __restrict__ mrows,
-                                                    uint32_t* __restrict__ m_out) {
+__global__ void __launch_bounds__(256, 2) k_crt_dec(KeyDev key, const uint32_t* __restrict__ Np, int64_t count,
+                                                    uint32_t* __restrict__ mrows, uint32_t* __restrict__ m_out) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP::TPI;
   if (e >= count) return;
   const int st = (int)count;
   uint32_t* rp = mrows + e;
   uint32_t* rq = mrows + (size_t)2 * MP::S4 * count + e;
   MP M;
-  M.init(key.p.N, key.p.n0inv);
+  M.init(Np, key.p.n0inv);
   uint32_t u[MP::L];
   M.load_strided(u, rp, st);
   M.add_sub_rows(u, key.p2x_lim, rq, st);
@@ -469,6 +473,7 @@ XHE_DEV void pow_window4(const M_& M, uint32_t (&b)[M_::L], const uint32_t* R1, 
     M.store_strided(one, tab, st);   // tab[0] = R (Montgomery one)
   }
   wave_sync_mem_();
+#pragma unroll 1
   for (int t = 2; t < 16; ++t) {
     M.mul(b, AStrided{tab + rs, st});
     M.store_strided(b, tab + rs * t, st);
@@ -907,16 +912,17 @@ __global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* 
 }
 
 // k_tab_chain: one group per window w, half = win/2. With B = tab[w][1]:
-//   tab[w][d]          = B^d            for d < 2^half          (low chain)
-//   tab[w][d << half]  = B^(d << half)  for 0 < d < 2^half      (high chain)
+//   tab[w][d]          = B^d            for d < 2^half              (low chain)
+//   tab[w][d << half]  = B^(d << half)  for 0 < d < 2^(win - half)  (high chain)
 // k_tab_combine then fills tab[w][hi|lo] = tab[w][hi] * tab[w][lo].
 template <class MP2>
-__global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, int win, int nwin, uint32_t* tab) {
+__global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, const uint32_t* __restrict__ Nm, int win, int nwin,
+                                                     uint32_t* __restrict__ tab) {
   const int w = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI);
   if (w >= nwin) return;
   MP2 M;
-  M.init(md.N, md.n0inv);
-  const int half = win / 2, lo_n = 1 << half;
+  M.init(Nm, md.n0inv);
+  const int half = win / 2, lo_n = 1 << half, hi_n = 1 << (win - half);
   uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
   uint32_t b[MP2::L];
   M.load_row(b, md.R1);
@@ -934,7 +940,7 @@ __global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, int win, int nwi
   const size_t gs = (size_t)lo_n * MP2::S4;  // row stride of the high chain
   M.store_row(b, t + gs);
   wave_sync_mem_();
-  for (int d = 2; d < lo_n; ++d) {
+  for (int d = 2; d < hi_n; ++d) {
     M.mul(b, ARow{t + gs});
     M.reduce_once(b);
     M.store_row(b, t + (size_t)d * gs);
@@ -942,7 +948,8 @@ __global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, int win, int nwi
 }
 
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, int win, int nwin, uint32_t* tab) {
+__global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, const uint32_t* __restrict__ Nm, int win,
+                                                         int nwin, uint32_t* __restrict__ tab) {
   const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   const int64_t rows = (int64_t)nwin << win;
   if (idx >= rows) return;
@@ -953,7 +960,7 @@ __global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, int win, int 
   if (lo == 0 || hi == 0) return;  // chain entries
   uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
   MP2 M;
-  M.init(md.N, md.n0inv);
+  M.init(Nm, md.n0inv);
   uint32_t b[MP2::L];
   M.load_row(b, t + ((size_t)hi << half) * MP2::S4);
   M.mul(b, ARow{t + (size_t)lo * MP2::S4});
