@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libxhe.so")
+LIB_PATH = os.environ.get("XHE_LIB", os.path.join(_HERE, "lib", "libxhe.so"))  # XHE_LIB: A/B builds
 
 XHE_OK = 0
 XHE_EINVAL = -1

@@ -219,24 +219,103 @@ struct Mont {
     }
 #undef XHE_MAC4_ASM
   }
+  // 8 limbs (16 mads) per statement: half the statement boundaries (each costs
+  // an s_nop the compiler puts after inline asm that writes vcc).
+  XHE_DEV void mac8(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, uint32_t m,
+                    int j) const {
+#define XHE_MAC8_ASM                         \
+  "v_mad_u64_u32 %0, vcc, %9, %11, %1\n\t"    \
+  "v_mad_u64_u32 %0, vcc, %10, %19, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %9, %12, %2\n\t"    \
+  "v_mad_u64_u32 %1, vcc, %10, %20, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %9, %13, %3\n\t"    \
+  "v_mad_u64_u32 %2, vcc, %10, %21, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %9, %14, %4\n\t"    \
+  "v_mad_u64_u32 %3, vcc, %10, %22, %3\n\t"  \
+  "v_mad_u64_u32 %4, vcc, %9, %15, %5\n\t"    \
+  "v_mad_u64_u32 %4, vcc, %10, %23, %4\n\t"  \
+  "v_mad_u64_u32 %5, vcc, %9, %16, %6\n\t"    \
+  "v_mad_u64_u32 %5, vcc, %10, %24, %5\n\t"  \
+  "v_mad_u64_u32 %6, vcc, %9, %17, %7\n\t"    \
+  "v_mad_u64_u32 %6, vcc, %10, %25, %6\n\t"  \
+  "v_mad_u64_u32 %7, vcc, %9, %18, %8\n\t"    \
+  "v_mad_u64_u32 %7, vcc, %10, %26, %7"
+    if constexpr (TPI == 1) {
+      asm(XHE_MAC8_ASM
+          : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4]),
+            "+v"(T[j + 5]), "+v"(T[j + 6])
+          : "v"(T[j + 7]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]),
+            "v"(b[j + 4]), "v"(b[j + 5]), "v"(b[j + 6]), "v"(b[j + 7]), "s"(Np[j]), "s"(Np[j + 1]),
+            "s"(Np[j + 2]), "s"(Np[j + 3]), "s"(Np[j + 4]), "s"(Np[j + 5]), "s"(Np[j + 6]), "s"(Np[j + 7])
+          : "vcc");
+    } else {
+      asm(XHE_MAC8_ASM
+          : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4]),
+            "+v"(T[j + 5]), "+v"(T[j + 6])
+          : "v"(T[j + 7]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]),
+            "v"(b[j + 4]), "v"(b[j + 5]), "v"(b[j + 6]), "v"(b[j + 7]), "v"(nl[j]), "v"(nl[j + 1]),
+            "v"(nl[j + 2]), "v"(nl[j + 3]), "v"(nl[j + 4]), "v"(nl[j + 5]), "v"(nl[j + 6]), "v"(nl[j + 7])
+          : "vcc");
+    }
+#undef XHE_MAC8_ASM
+  }
 
-  // One column of the product: T <- (T + a_i*b + m*N) / 2^W
-  XHE_DEV void step(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, bool lead) const {
-    uint64_t x0 = mad64(ai, b[0], T[0]);
-    uint32_t m = ((uint32_t)x0 * n0inv) & MASK;
-    m = G::bcast0(m);
+  // One column of the product: T <- (T + a_i*b + m*N) / 2^W, software-
+  // pipelined: on entry x0 = a_i*b[0] + T[0] and m (its Montgomery digit) are
+  // already known; as soon as the first block has produced the new T[0] the
+  // next column's x0 and m are formed, so the mul_lo -> and -> broadcast chain
+  // overlaps the remaining mads instead of stalling the start of every column.
+  XHE_DEV void step(const uint32_t* Np, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, uint32_t ai_next,
+                    uint32_t& m, uint64_t& x0, bool lead) const {
+    static_assert(L >= 5, "pipelined step needs L >= 5");
+    // The next column's chain (carry into T[0] -> x0' -> x0' * n0inv -> mask +
+    // broadcast) is dependent end to end, and a wave issues in order: each
+    // link is placed after its own block of independent mads (sched_barrier)
+    // so its latency is covered instead of stalling the wave.
+    uint64_t xn = 0;
+    uint32_t t = 0, mn = 0;
+    int stage = 0;
+    auto advance = [&]() {
+      // (the empty volatile asm pins each link between its barriers; plain
+      // arithmetic would otherwise be sunk to its use at IR level)
+      if (stage == 0) {
+        T[0] += lead ? (x0 >> W) : 0ull;
+        asm volatile("" : "+v"(T[0]));
+      } else if (stage == 1) {
+        xn = mad64(ai_next, b[0], T[0]);
+        asm volatile("" : "+v"(xn));
+      } else if (stage == 2) {
+        t = (uint32_t)xn * n0inv;
+        asm volatile("" : "+v"(t));
+      } else if (stage == 3) {
+        mn = G::bcast0(t & MASK);
+        asm volatile("" : "+v"(mn));
+      }
+      ++stage;
+      __builtin_amdgcn_sched_barrier(0);
+    };
     x0 = madN(Np, m, 0, x0);
-    // 4 limbs (8 mads) per asm statement: hipcc separates inline-asm
-    // statements with s_nop, so one statement per mad would cost an issue slot
-    // per mad. Outputs are early-clobber so T[j-1] can reuse its own dead
-    // register (no register rotation / back-edge copies).
-    int j = 1;
+    mac4(Np, T, b, ai, m, 1);
+    advance();
+    int j = 5;
 #pragma unroll
-    for (; j + 4 <= L; j += 4) mac4(Np, T, b, ai, m, j);
+    for (; j + 8 <= L; j += 8) {
+      mac8(Np, T, b, ai, m, j);
+      if (stage < 4) advance();
+    }
+#pragma unroll
+    for (; j + 4 <= L; j += 4) {
+      mac4(Np, T, b, ai, m, j);
+      if (stage < 4) advance();
+    }
 #pragma unroll
     for (; j < L; ++j) T[j - 1] = madN(Np, m, j, mad64(ai, b[j], T[j]));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (stage < 4) advance();
     T[L - 1] = G::from_next64(x0);
-    T[0] += lead ? (x0 >> W) : 0ull;
+    x0 = xn;
+    m = mn;
   }
 
   // Carry-normalise the accumulators into W-bit limbs.
@@ -282,22 +361,25 @@ struct Mont {
     const bool lead = G::g() == 0;
     const uint32_t* Np = np();
     uint4 cur = a.load4(0);
+    uint64_t x0 = mad64(cur.x, b[0], T[0]);
+    uint32_t m = G::bcast0(((uint32_t)x0 * n0inv) & MASK);
     int i = 0;
     for (; i + 4 <= S; i += 4) {
       uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
       __builtin_amdgcn_sched_barrier(0);
-      step(Np, T, b, cur.x, lead);
+      step(Np, T, b, cur.x, cur.y, m, x0, lead);
       __builtin_amdgcn_sched_barrier(0);
-      step(Np, T, b, cur.y, lead);
+      step(Np, T, b, cur.y, cur.z, m, x0, lead);
       __builtin_amdgcn_sched_barrier(0);
-      step(Np, T, b, cur.z, lead);
+      step(Np, T, b, cur.z, cur.w, m, x0, lead);
       __builtin_amdgcn_sched_barrier(0);
-      step(Np, T, b, cur.w, lead);
+      step(Np, T, b, cur.w, nxt.x, m, x0, lead);
       __builtin_amdgcn_sched_barrier(0);
       cur = nxt;
     }
 #pragma unroll
-    for (int r = 0; r < (S & 3); ++r) step(Np, T, b, comp4(cur, r), lead);
+    for (int r = 0; r < (S & 3); ++r)
+      step(Np, T, b, comp4(cur, r), r + 1 < (S & 3) ? comp4(cur, r + 1) : 0u, m, x0, lead);
   }
 
   // Montgomery reduction of a double-length value: lo = limbs [0,S) in b,
