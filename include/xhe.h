@@ -94,7 +94,23 @@ int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_
 int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev, int dmax, int64_t count,
                 const int64_t* seg_begin, int64_t nseg, uint32_t* out_dev, void* stream);
 
+/* Encrypted matrix-vector product as a multi-exponentiation: the object-dtype
+ * np.matmul(enc[B], X[B, D]) of logistic_regression/trainer.py:166 (and
+ * linear_regression/trainer.py:207, poisson_regression/trainer.py:267,
+ * pearson/trainer.py:120-123), i.e. per column j the fold of
+ * PaillierCiphertext.__mul__ + __add__ (paillier.py:106-187), is
+ *   out[j] = prod_{t < nterms} bases[idx[j*nterms + t]]^k[j*nterms + t] mod n^2
+ * with the caller folding signs (base = c or c^-1, xhe_invert) and exponent
+ * alignment (k << (e - e_min)) into idx/k. k: kw words per term, < 2^kbits.
+ * Straus windows of win_bits (0 = chosen to minimise products) with per-base
+ * tables shared by all columns. */
+int xhe_multiexp(const xhe_key* key, const uint32_t* bases_dev, int64_t nbases, const int32_t* idx_dev,
+                 const uint32_t* k_dev, int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits,
+                 uint32_t* out_dev, void* stream);
+
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
+int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* k,
+                      int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits, uint32_t* out);
 int xhe_segprod_host(const xhe_key* key, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
                      const int64_t* seg_begin, int64_t nseg, uint32_t* out);
 int xhe_mulmod_host(const xhe_key* key, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,

@@ -47,6 +47,10 @@ SIGNATURES = {
                                        _vp]),
     "xhe_segprod": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp]),
     "xhe_segprod_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int64, _vp, ctypes.c_int64, _vp]),
+    "xhe_multiexp": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.c_int, _vp, _vp]),
+    "xhe_multiexp_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp]),
     "xhe_encrypt_host": (ctypes.c_int, [_vp, _u32p, _u32p, ctypes.c_int64, _u32p]),
     "xhe_decrypt_host": (ctypes.c_int, [_vp, _u32p, ctypes.c_int64, _u32p]),
     "xhe_encrypt_f64_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -27,19 +27,26 @@ def needs_build():
     return any(os.path.getmtime(s) > t for s in SOURCES)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile libxhe.so. `out`/`defines` build A/B variants of the kernels
+    (e.g. defines=["XHE_NPIPE=0"], loaded through $XHE_LIB)."""
+    lib = out or LIB
+    if not force and out is None and not defines and not needs_build():
         return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           os.path.join(CSRC, "xhe.hip"), "-o", tmp]
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    tmp = lib + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared"]
+    cmd += [f"-D{d}" for d in defines]
+    cmd += [os.path.join(CSRC, "xhe.hip"), "-o", tmp]
     if verbose:
         print("[xfl_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    args = sys.argv[1:]
+    out = args[args.index("--out") + 1] if "--out" in args else None
+    defs = [args[i + 1] for i, a in enumerate(args) if a == "-D"]
+    build(force="--force" in args, out=out, defines=defs)

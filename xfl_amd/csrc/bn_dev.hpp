@@ -24,6 +24,14 @@ namespace xhe {
 
 #define XHE_DEV __device__ __forceinline__
 
+// Build switches (A/B measurement; defaults are the measured-best variant)
+#ifndef XHE_NPIPE
+#define XHE_NPIPE 1  // TPI==1: modulus limbs loaded one block ahead (Mont::step1)
+#endif
+#ifndef XHE_MAC_SPLIT
+#define XHE_MAC_SPLIT 1  // a*b mads of a block before its m*N mads
+#endif
+
 // d = a*b + c with one v_mad_u64_u32. Inline asm keeps a and b 32-bit: the
 // C form (uint64_t)a*b + c makes the compiler hold every limb as a
 // zero-extended 64-bit register pair, doubling the resident operand.
@@ -260,6 +268,163 @@ struct Mont {
 #undef XHE_MAC8_ASM
   }
 
+  // ---- TPI == 1 with the modulus limbs in SGPRs loaded one block ahead.
+  // Loading N[j..j+7] right before the block that uses it exposes the scalar
+  // load latency at every block (an s_waitcnt lgkmcnt(0) per block, five per
+  // column); here each block's limbs are requested one block earlier, and the
+  // limbs of the first and last blocks of a column stay resident for the
+  // whole product.
+  static constexpr int J8 = 5 + ((L - 5) / 8) * 8;  // first limb after the 8-limb blocks
+  static constexpr int TL = L - J8;                 // tail limbs (0..7)
+  struct NRes {
+    uint32_t n0, h[4], f[8], t[8];  // N[0], N[1..4], N[5..12], N[J8..L)
+  };
+  XHE_DEV void load_res(const uint32_t* Np, NRes& r) const {
+    r.n0 = Np[0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.h[k] = Np[1 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.f[k] = Np[5 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.t[k] = k < TL ? Np[J8 + k] : 0u;
+  }
+#if XHE_MAC_SPLIT
+  // all a_i*b products of the block first, then the m*N products: each m*N
+  // mad reads an accumulator written 4 (8) instructions earlier instead of
+  // by the instruction right before it
+#define XHE_MAC4V_ASM                       \
+  "v_mad_u64_u32 %0, vcc, %5, %7, %1\n\t"   \
+  "v_mad_u64_u32 %1, vcc, %5, %8, %2\n\t"   \
+  "v_mad_u64_u32 %2, vcc, %5, %9, %3\n\t"   \
+  "v_mad_u64_u32 %3, vcc, %5, %10, %4\n\t"  \
+  "v_mad_u64_u32 %0, vcc, %6, %11, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %6, %12, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %6, %13, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %6, %14, %3"
+#define XHE_MAC8V_ASM                        \
+  "v_mad_u64_u32 %0, vcc, %9, %11, %1\n\t"   \
+  "v_mad_u64_u32 %1, vcc, %9, %12, %2\n\t"   \
+  "v_mad_u64_u32 %2, vcc, %9, %13, %3\n\t"   \
+  "v_mad_u64_u32 %3, vcc, %9, %14, %4\n\t"   \
+  "v_mad_u64_u32 %4, vcc, %9, %15, %5\n\t"   \
+  "v_mad_u64_u32 %5, vcc, %9, %16, %6\n\t"   \
+  "v_mad_u64_u32 %6, vcc, %9, %17, %7\n\t"   \
+  "v_mad_u64_u32 %7, vcc, %9, %18, %8\n\t"   \
+  "v_mad_u64_u32 %0, vcc, %10, %19, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %10, %20, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %10, %21, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %10, %22, %3\n\t"  \
+  "v_mad_u64_u32 %4, vcc, %10, %23, %4\n\t"  \
+  "v_mad_u64_u32 %5, vcc, %10, %24, %5\n\t"  \
+  "v_mad_u64_u32 %6, vcc, %10, %25, %6\n\t"  \
+  "v_mad_u64_u32 %7, vcc, %10, %26, %7"
+#else
+#define XHE_MAC4V_ASM                       \
+  "v_mad_u64_u32 %0, vcc, %5, %7, %1\n\t"   \
+  "v_mad_u64_u32 %0, vcc, %6, %11, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %5, %8, %2\n\t"   \
+  "v_mad_u64_u32 %1, vcc, %6, %12, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %5, %9, %3\n\t"   \
+  "v_mad_u64_u32 %2, vcc, %6, %13, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %5, %10, %4\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %6, %14, %3"
+#define XHE_MAC8V_ASM                        \
+  "v_mad_u64_u32 %0, vcc, %9, %11, %1\n\t"   \
+  "v_mad_u64_u32 %0, vcc, %10, %19, %0\n\t"  \
+  "v_mad_u64_u32 %1, vcc, %9, %12, %2\n\t"   \
+  "v_mad_u64_u32 %1, vcc, %10, %20, %1\n\t"  \
+  "v_mad_u64_u32 %2, vcc, %9, %13, %3\n\t"   \
+  "v_mad_u64_u32 %2, vcc, %10, %21, %2\n\t"  \
+  "v_mad_u64_u32 %3, vcc, %9, %14, %4\n\t"   \
+  "v_mad_u64_u32 %3, vcc, %10, %22, %3\n\t"  \
+  "v_mad_u64_u32 %4, vcc, %9, %15, %5\n\t"   \
+  "v_mad_u64_u32 %4, vcc, %10, %23, %4\n\t"  \
+  "v_mad_u64_u32 %5, vcc, %9, %16, %6\n\t"   \
+  "v_mad_u64_u32 %5, vcc, %10, %24, %5\n\t"  \
+  "v_mad_u64_u32 %6, vcc, %9, %17, %7\n\t"   \
+  "v_mad_u64_u32 %6, vcc, %10, %25, %6\n\t"  \
+  "v_mad_u64_u32 %7, vcc, %9, %18, %8\n\t"   \
+  "v_mad_u64_u32 %7, vcc, %10, %26, %7"
+#endif
+  XHE_DEV void mac4v(uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, uint32_t m, int j,
+                     const uint32_t* n) const {
+    asm(XHE_MAC4V_ASM
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2])
+        : "v"(T[j + 3]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]), "s"(n[0]),
+          "s"(n[1]), "s"(n[2]), "s"(n[3])
+        : "vcc");
+  }
+  XHE_DEV void mac8v(uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai, uint32_t m, int j,
+                     const uint32_t* n) const {
+    asm(XHE_MAC8V_ASM
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4]),
+          "+v"(T[j + 5]), "+v"(T[j + 6])
+        : "v"(T[j + 7]), "v"(ai), "v"(m), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]), "v"(b[j + 4]),
+          "v"(b[j + 5]), "v"(b[j + 6]), "v"(b[j + 7]), "s"(n[0]), "s"(n[1]), "s"(n[2]), "s"(n[3]), "s"(n[4]),
+          "s"(n[5]), "s"(n[6]), "s"(n[7])
+        : "vcc");
+  }
+
+  // step() for TPI == 1 (same schedule; N from R and the block pipeline)
+  XHE_DEV void step1(const uint32_t* Np, const NRes& R, uint64_t (&T)[L], const uint32_t (&b)[L], uint32_t ai,
+                     uint32_t ai_next, uint32_t& m, uint64_t& x0, bool lead) const {
+    static_assert(L >= 13, "step1 needs at least one 8-limb block");
+    uint64_t xn = 0;
+    uint32_t t = 0, mn = 0;
+    int stage = 0;
+    auto advance = [&]() {
+      if (stage == 0) {
+        T[0] += lead ? (x0 >> W) : 0ull;
+        asm volatile("" : "+v"(T[0]));
+      } else if (stage == 1) {
+        xn = mad64(ai_next, b[0], T[0]);
+        asm volatile("" : "+v"(xn));
+      } else if (stage == 2) {
+        t = (uint32_t)xn * n0inv;
+        asm volatile("" : "+v"(t));
+      } else if (stage == 3) {
+        mn = t & MASK;
+        asm volatile("" : "+v"(mn));
+      }
+      ++stage;
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    uint32_t nb[2][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nb[0][k] = R.f[k];
+    x0 = mad64s(m, R.n0, x0);
+    mac4v(T, b, ai, m, 1, R.h);
+    advance();
+#pragma unroll
+    for (int blk = 0; blk < (J8 - 5) / 8; ++blk) {
+      const int j = 5 + 8 * blk;
+      const int cur = blk & 1;
+      if (j + 16 <= J8) {
+        // Scalar loads return out of order, so the only wait is lgkmcnt(0):
+        // consume this block's limbs first (the wait lands here, covering
+        // only the load issued one block ago), then request the next block's.
+        asm volatile("" ::"s"(nb[cur][0]), "s"(nb[cur][1]), "s"(nb[cur][2]), "s"(nb[cur][3]), "s"(nb[cur][4]),
+                     "s"(nb[cur][5]), "s"(nb[cur][6]), "s"(nb[cur][7]));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nb[cur ^ 1][k] = Np[j + 8 + k];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mac8v(T, b, ai, m, j, nb[cur]);
+      if (stage < 4) advance();
+      else __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (TL >= 4) mac4v(T, b, ai, m, J8, R.t);
+#pragma unroll
+    for (int k = (TL >= 4 ? 4 : 0); k < TL; ++k) T[J8 + k - 1] = mad64s(m, R.t[k], mad64(ai, b[J8 + k], T[J8 + k]));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (stage < 4) advance();
+    T[L - 1] = 0;
+    x0 = xn;
+    m = mn;
+  }
+
   // One column of the product: T <- (T + a_i*b + m*N) / 2^W, software-
   // pipelined: on entry x0 = a_i*b[0] + T[0] and m (its Montgomery digit) are
   // already known; as soon as the first block has produced the new T[0] the
@@ -364,6 +529,29 @@ struct Mont {
     uint64_t x0 = mad64(cur.x, b[0], T[0]);
     uint32_t m = G::bcast0(((uint32_t)x0 * n0inv) & MASK);
     int i = 0;
+#if XHE_NPIPE
+    if constexpr (TPI == 1 && L >= 13) {
+      NRes R;
+      load_res(Np, R);
+      for (; i + 4 <= S; i += 4) {
+        uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.x, cur.y, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.y, cur.z, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.z, cur.w, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.w, nxt.x, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        cur = nxt;
+      }
+#pragma unroll
+      for (int r = 0; r < (S & 3); ++r)
+        step1(Np, R, T, b, comp4(cur, r), r + 1 < (S & 3) ? comp4(cur, r + 1) : 0u, m, x0, lead);
+      return;
+    }
+#endif
     for (; i + 4 <= S; i += 4) {
       uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
       __builtin_amdgcn_sched_barrier(0);

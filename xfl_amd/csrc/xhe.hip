@@ -535,27 +535,19 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   return XHE_OK;
 }
 
-// Segmented modular product: out[s] = prod_{i in seg s} c_i^(2^d_i) mod n^2.
-// seg_begin: nseg+1 offsets into the (already segment-ordered) inputs.
+// Reduce segment-ordered Montgomery rows [S4][count] to one row per segment
+// (seg: nseg+1 offsets) by levels of k_chunk_prod (C rows per chunk). Takes
+// ownership of `rows`; returns a new [S4][nseg] buffer (hipFree by the
+// caller); an empty segment yields the Montgomery one.
 template <class Sh>
-void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
-                  const int64_t* seg_begin_host, int64_t nseg, uint32_t* out, hipStream_t s) {
+uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s) {
   using MN2 = typename Sh::MN2;
   const int S4 = MN2::S4;
   const int64_t C = 32;  // chunk length per level
+  const int64_t nseg = (int64_t)seg.size() - 1;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
-  uint32_t *rows = nullptr, *sq = nullptr;
-  HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
-  HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
-  if (count > 0) {
-    hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, d, count, dmax,
-                       rows, sq);
-    HIPCHK(hipGetLastError());
-  }
-  std::vector<int64_t> seg(seg_begin_host, seg_begin_host + nseg + 1);
   int64_t n_cur = count;
   uint32_t* cur = rows;
-  std::vector<uint32_t*> to_free{sq};
   while (true) {
     bool done = true;
     for (int64_t i = 0; i < nseg; ++i)
@@ -585,11 +577,90 @@ void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dma
     seg = nseg_b;
     if (done) break;
   }
+  return cur;
+}
+
+// Segmented modular product: out[s] = prod_{i in seg s} c_i^(2^d_i) mod n^2.
+// seg_begin: nseg+1 offsets into the (already segment-ordered) inputs.
+template <class Sh>
+void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
+                  const int64_t* seg_begin_host, int64_t nseg, uint32_t* out, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  const int S4 = MN2::S4;
+  auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
+  uint32_t *rows = nullptr, *sq = nullptr;
+  HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+  HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+  if (count > 0) {
+    hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, d, count, dmax,
+                       rows, sq);
+    HIPCHK(hipGetLastError());
+  }
+  uint32_t* cur = reduce_segments<Sh>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s);
   hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, k->kd.n2.N, cur, nseg, out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(cur);
-  for (auto p : to_free) (void)hipFree(p);
+  (void)hipFree(sq);
+}
+
+// Window bits for a multi-exponentiation: minimise table products
+// nbases*(2^c - 2) plus gathered products ncols*nterms*ceil(kbits/c), with the
+// tables capped at ~2 GiB.
+int mexp_window(int64_t nbases, int64_t ncols, int64_t nterms, int kbits, int s4) {
+  int best = 1;
+  double best_cost = 1e300;
+  for (int c = 1; c <= 8; ++c) {
+    if (c > 1 && (double)(nbases << c) * s4 * 4 > 2147483648.0) break;
+    double cost = (double)nbases * ((1 << c) - 2) + (double)ncols * nterms * ((kbits + c - 1) / c) +
+                  (double)ncols * kbits;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+// Multi-exponentiation out[j] = prod_t bases[idx[j][t]]^k[j][t] mod n^2.
+template <class Sh>
+void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* kx,
+                   int kw, int kbits, int64_t ncols, int64_t nterms, int c, uint32_t* out, hipStream_t s) {
+  using MN2 = typename Sh::MN2;
+  const int S4 = MN2::S4;
+  auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
+  const int nwin = std::max(1, (kbits + c - 1) / c);
+  uint32_t *tab = nullptr, *rows = nullptr, *sq = nullptr;
+  HIPCHK(hipMallocAsync((void**)&tab, ((size_t)nbases << c) * S4 * 4, s));
+  {
+    ProfScope ps("k_mexp_tab", s);
+    hipLaunchKernelGGL(k_mexp_tab<MN2>, blocks(nbases), dim3(256), 0, s, k->kd, k->kd.n2.N, bases, nbases, c, tab);
+    HIPCHK(hipGetLastError());
+  }
+  // enough lane groups to fill the chip, at least 2 terms per group
+  const int64_t segs = ncols * nwin;
+  const int64_t target_groups = 32768;
+  const int64_t chunk = std::max<int64_t>(2, std::min<int64_t>(64, (segs * nterms + target_groups - 1) / target_groups));
+  const int64_t nchunks = (nterms + chunk - 1) / chunk;
+  const int64_t n_out = segs * nchunks;
+  HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * n_out * 4, s));
+  {
+    ProfScope ps("k_mexp_gather", s);
+    hipLaunchKernelGGL(k_mexp_gather<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, k->kd.n2.N, tab, c, idx, kx, kw,
+                       nterms, nwin, nchunks, chunk, n_out, rows);
+    HIPCHK(hipGetLastError());
+  }
+  std::vector<int64_t> seg(segs + 1);
+  for (int64_t i = 0; i <= segs; ++i) seg[i] = i * nchunks;
+  uint32_t* P = reduce_segments<Sh>(k, rows, n_out, std::move(seg), s);
+  HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * ncols * 4, s));
+  hipLaunchKernelGGL(k_mexp_horner<MN2>, blocks(ncols), dim3(256), 0, s, k->kd, k->kd.n2.N, P, nwin, c, ncols, sq,
+                     out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(tab);
+  (void)hipFree(P);
+  (void)hipFree(sq);
 }
 
 template <class Sh>
@@ -1071,6 +1142,51 @@ int xhe_segprod_host(const xhe_key* key, const uint32_t* c, const int32_t* d, in
                          dout.as<uint32_t>(), st.s);
     if (rc != XHE_OK) return rc;
     HIPCHK(hipMemcpyAsync(out, dout.p, (size_t)nseg * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
+    HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_multiexp(const xhe_key* key, const uint32_t* bases_dev, int64_t nbases, const int32_t* idx_dev,
+                 const uint32_t* k_dev, int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits,
+                 uint32_t* out_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (!key || nbases <= 0 || ncols <= 0 || nterms <= 0 || !bases_dev || !idx_dev || !k_dev || !out_dev || kw <= 0 ||
+        kbits < 0 || kbits > 32 * kw || win_bits < 0 || win_bits > 8)
+      return fail(XHE_EINVAL, "xhe_multiexp: bad argument");
+    if (ncols * nterms > (int64_t)1 << 31 || nbases > (int64_t)1 << 30)
+      return fail(XHE_EINVAL, "xhe_multiexp: problem too large for one call");
+    DevGuard dg(key->device);
+    const int s4 = key->K == 2048 ? Shape2048::MN2::S4 : Shape3072::MN2::S4;
+    const int c = win_bits ? win_bits : mexp_window(nbases, ncols, nterms, std::max(kbits, 1), s4);
+    if (key->K == 2048)
+      multiexp_impl<Shape2048>(key, bases_dev, nbases, idx_dev, k_dev, kw, std::max(kbits, 1), ncols, nterms, c,
+                               out_dev, (hipStream_t)stream);
+    else
+      multiexp_impl<Shape3072>(key, bases_dev, nbases, idx_dev, k_dev, kw, std::max(kbits, 1), ncols, nterms, c,
+                               out_dev, (hipStream_t)stream);
+    return XHE_OK;
+  });
+}
+
+int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* k,
+                      int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits, uint32_t* out) {
+  return guarded([&]() -> int {
+    if (!key || nbases <= 0 || ncols <= 0 || nterms <= 0 || !bases || !idx || !k || !out || kw <= 0)
+      return fail(XHE_EINVAL, "xhe_multiexp_host: bad argument");
+    for (int64_t i = 0; i < ncols * nterms; ++i)
+      if (idx[i] < 0 || idx[i] >= nbases) return fail(XHE_EINVAL, "xhe_multiexp_host: base index out of range");
+    DevGuard dg(key->device);
+    Stream st;
+    DevBuf db((size_t)nbases * key->n2w * 4, st.s), di((size_t)ncols * nterms * 4, st.s),
+        dk((size_t)ncols * nterms * kw * 4, st.s), dout((size_t)ncols * key->n2w * 4, st.s);
+    HIPCHK(hipMemcpyAsync(db.p, bases, (size_t)nbases * key->n2w * 4, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(di.p, idx, (size_t)ncols * nterms * 4, hipMemcpyHostToDevice, st.s));
+    HIPCHK(hipMemcpyAsync(dk.p, k, (size_t)ncols * nterms * kw * 4, hipMemcpyHostToDevice, st.s));
+    int rc = xhe_multiexp(key, db.as<uint32_t>(), nbases, di.as<int32_t>(), dk.as<uint32_t>(), kw, kbits, ncols, nterms,
+                          win_bits, dout.as<uint32_t>(), st.s);
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipMemcpyAsync(out, dout.p, (size_t)ncols * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
     HIPCHK(hipStreamSynchronize(st.s));
     return XHE_OK;
   });

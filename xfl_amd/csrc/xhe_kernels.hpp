@@ -887,6 +887,98 @@ __global__ void k_inv_to_row(KeyDev key, const uint32_t* __restrict__ Nn2, const
   M.store_row(b, row);
 }
 
+// ---- multi-exponentiation (encrypted mat-vec, np.matmul(enc[B], X[B, D]),
+// logistic_regression/trainer.py:166): out[j] = prod_t base[idx[j][t]]^k[j][t].
+// Straus-style with per-base window tables shared by every column and a
+// parallel product per window:
+//   P[j][w] = prod_t tab[idx[j][t]][digit_w(k[j][t])]   (k_mexp_gather + k_chunk_prod)
+//   out[j]  = Horner over w: acc = acc^(2^c) * P[j][w]   (k_mexp_horner)
+// Tables: tab[b][d] = base_b^d * R mod n^2, d < 2^c, rows of S4 words.
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_mexp_tab(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                     const uint32_t* __restrict__ bases, int64_t nbases, int c,
+                                                     uint32_t* __restrict__ tab) {
+  const int64_t bi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (bi >= nbases) return;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t* t = tab + ((size_t)bi << c) * MN2::S4;
+  uint32_t b[MN2::L];
+  M.load_row(b, key.n2.R1);
+  M.reduce_once(b);
+  M.store_row(b, t);  // base^0 = R
+  M.load_words(b, bases + (size_t)bi * key.n2w, key.n2w);
+  M.mul(b, ARow{key.n2.R2});
+  M.reduce_once(b);
+  M.store_row(b, t + MN2::S4);
+  wave_sync_mem_();
+  const int rows = 1 << c;
+  for (int d = 2; d < rows; ++d) {
+    M.mul(b, ARow{t + MN2::S4});
+    M.reduce_once(b);
+    M.store_row(b, t + (size_t)d * MN2::S4);
+  }
+}
+
+// One lane group per (segment s = j*nwin + w, chunk t): the product of the
+// chunk's table rows, stored as a Montgomery row of out [S4][n_out] at
+// column s*nchunks + t (the segment order k_chunk_prod reduces).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_mexp_gather(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                        const uint32_t* __restrict__ tab, int c,
+                                                        const int32_t* __restrict__ idx,
+                                                        const uint32_t* __restrict__ kx, int kw, int64_t nterms,
+                                                        int nwin, int64_t nchunks, int64_t chunk, int64_t n_out,
+                                                        uint32_t* __restrict__ out) {
+  const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (g >= n_out) return;
+  const int64_t s = g / nchunks, t = g - s * nchunks;
+  const int64_t j = s / nwin;
+  const int w = (int)(s - j * nwin);
+  const int64_t lo = t * chunk, hi = lo + chunk < nterms ? lo + chunk : nterms;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  const int32_t* ij = idx + j * nterms;
+  const uint32_t* kj = kx + (size_t)j * nterms * kw;
+  auto row = [&](int64_t i) {
+    uint32_t d = digit_at(kj + (size_t)i * kw, kw, w * c, c);
+    return tab + (((size_t)ij[i] << c) + d) * MN2::S4;
+  };
+  M.load_row(b, row(lo));
+  for (int64_t i = lo + 1; i < hi; ++i) M.mul(b, ARow{row(i)});
+  M.reduce_once(b);
+  M.store_strided(b, out + g, (int)n_out);
+}
+
+// out[j] = prod_w P[j][w]^(2^(c*w)), P rows [S4][ncols*nwin] (column j*nwin+w);
+// sq: one scratch row per column ([S4][ncols]).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_mexp_horner(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                        const uint32_t* __restrict__ P, int nwin, int c,
+                                                        int64_t ncols, uint32_t* __restrict__ sq,
+                                                        uint32_t* __restrict__ out) {
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (j >= ncols) return;
+  const int pst = (int)(ncols * nwin);
+  const int st = (int)ncols;
+  MN2 M;
+  M.init(Nn2, key.n2.n0inv);
+  uint32_t b[MN2::L];
+  M.load_strided(b, P + j * nwin + (nwin - 1), pst);
+  for (int w = nwin - 2; w >= 0; --w) {
+    for (int r = 0; r < c; ++r) {
+      M.store_strided(b, sq + j, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq + j, st});
+    }
+    M.mul(b, AStrided{P + j * nwin + w, pst});
+  }
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  store_packed(M, b, sq + j, st, out + (size_t)j * key.n2w, key.n2w);
+}
+
 // ============================================================== tables
 // Fixed-base table for h (Montgomery form row `hM`, canonical):
 //   tab[w][d] = h^(d * 2^(win*w)) * R mod M, d in [0, 2^win)

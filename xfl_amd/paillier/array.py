@@ -222,17 +222,17 @@ def _matmul(a, b):
             ex[i, j] = A[i].exponent + e
     emin = ex.min(axis=0)
     need_inv = [i for i in range(Bn) if any(neg[i])]
-    inv = {}
+    # bases: the B ciphertexts, then the inverses of those with a negative scalar
+    bases = [A[i].raw_ciphertext for i in range(Bn)]
+    inv_slot = {}
     if need_inv:
         r = ops.powmod(ctx, [A[i].raw_ciphertext for i in need_inv], [1] * len(need_inv), invert_first=True)
-        inv = dict(zip(need_inv, r))
-    bases, exps = [], []
-    for j in range(D):
-        for i in range(Bn):
-            bases.append(inv[i] if neg[i][j] else A[i].raw_ciphertext)
-            exps.append(ks[i][j] << int(ex[i, j] - emin[j]))
-    terms = ops.powmod(ctx, bases, exps)
-    r, _ = ops.segment_sums(ctx, terms, [0] * len(terms), [j * Bn for j in range(D + 1)])
+        for i, v in zip(need_inv, r):
+            inv_slot[i] = len(bases)
+            bases.append(v)
+    idx = [[inv_slot[i] if neg[i][j] else i for i in range(Bn)] for j in range(D)]
+    exps = [[ks[i][j] << int(ex[i, j] - emin[j]) for i in range(Bn)] for j in range(D)]
+    r = ops.multiexp(ctx, bases, idx, exps)
     out = np.empty(D, dtype=object)
     for j in range(D):
         out[j] = CT(ctx, r[j], int(emin[j]))

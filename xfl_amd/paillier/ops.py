@@ -151,6 +151,26 @@ def obfuscate(ctx, raws):
     return r
 
 
+def multiexp(ctx, bases, idx, ks, win_bits=0):
+    """out[j] = prod_t bases[idx[j][t]]^ks[j][t] mod n^2 (ks >= 0): one
+    xhe_multiexp call (Straus windows, per-base tables shared by all j)."""
+    dk = ctx.device_key()
+    ncols = len(idx)
+    nterms = len(idx[0]) if ncols else 0
+    if ncols == 0 or nterms == 0 or not bases:
+        raise ValueError("multiexp: empty problem")
+    flat_k = [int(k) for row in ks for k in row]
+    kbits = max(1, max(k.bit_length() for k in flat_k))
+    kw = (kbits + 31) // 32
+    bw = nat.ints_to_words(bases, dk.n2w)
+    iw = np.ascontiguousarray(idx, dtype=np.int32).reshape(ncols, nterms)
+    kwds = nat.ints_to_words(flat_k, kw)
+    out = np.empty((ncols, dk.n2w), dtype=np.uint32)
+    nat.check(nat.lib().xhe_multiexp_host(dk.handle, _vp(bw), len(bases), _vp(iw), _vp(kwds), kw, kbits, ncols,
+                                          nterms, int(win_bits), _vp(out)), "multiexp")
+    return nat.words_to_ints(out)
+
+
 def segment_sums(ctx, raws, exps, seg_begin):
     """Homomorphic sums of consecutive segments: segment s covers
     [seg_begin[s], seg_begin[s+1]); result exponent = min exponent of the
