@@ -82,6 +82,22 @@ def cpu_baseline(bits, seconds, cores):
                       f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
 
 
+def pmc_traffic(win, n):
+    """HBM bytes per k_djn_pow launch from the committed rocprofv3 PMC passes
+    (tools/profile_box.sh -> tools/pmc_traffic.py), when they were taken on
+    this configuration; else None. Counters cannot be read inside this run
+    (rocprofv3 --pmc is its own pass)."""
+    path = os.path.join(ROOT, "profiles", "r1", "k_djn_pow_pmc.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("win") != win or rec.get("n") != n or "traffic_bytes" not in rec:
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(path, ROOT)
+
+
 def _timed(fn, reps=3):
     """Average seconds per call of fn() on the current stream (1 untimed warm call)."""
     import torch
@@ -164,7 +180,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
     ap.add_argument("--key-bits", type=int, default=2048)
-    ap.add_argument("--win", type=int, default=20, help="fixed-base window bits (20: 2 x 16 GB tables)")
+    ap.add_argument("--win", type=int, default=22, help="fixed-base window bits (22: 2 x 57 GB tables, 47 products per prime)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
@@ -196,31 +212,52 @@ def main():
     ex = torch.empty(N, dtype=torch.int32, device="cuda")
     st = torch.empty(N, dtype=torch.int32, device="cuda")
     rnd = torch.empty((N, dk.rand_words), dtype=torch.int32, device="cuda")
-    ct = torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda")
-    gathered = torch.empty((world * N, dk.n2w), dtype=torch.int32, device="cuda") if world > 1 else None
+    # N > 1: ciphertext shards and gathered vectors are double-buffered so the
+    # all-gather of step i (RCCL's stream) overlaps the kernels of step i+1
+    nb = 2 if world > 1 else 1
+    cts = [torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda") for _ in range(nb)]
+    gathered = [torch.empty((world * N, dk.n2w), dtype=torch.int32, device="cuda") for _ in range(nb)] \
+        if world > 1 else None
+    pending = [None] * nb
     seed32 = os.urandom(32)
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(i):
+        b = i % nb
+        if pending[b] is not None:  # the gather still reading cts[b] must finish before it is rewritten
+            pending[b].wait()
+            pending[b] = None
+        ct = cts[b]
         nat.check(L.xhe_encode_f64(dk.handle, x.data_ptr(), N, 7, 0, 0, m.data_ptr(), ex.data_ptr(),
                                    st.data_ptr(), stream), "encode")
         nat.check(L.xhe_rand(dk.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
         nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
         if world > 1:
-            dist.all_gather_into_tensor(gathered, ct)
+            pending[b] = dist.all_gather_into_tensor(gathered[b], ct, async_op=True)
+        return ct
 
-    for i in range(args.warmup):
-        step(1_000_000 + i)
+    def drain():
+        for b in range(nb):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
+
+    last = 1_000_000 + max(args.warmup, 1) - 1  # the parity check below needs one finished step
+    for i in range(1_000_000, last + 1):
+        ct = step(i)
+    drain()
     torch.cuda.synchronize()
     # parity spot check of this rank's output against the oracle (not timed)
     from oracle import paillier_oracle as O
     okey = O.derive_private(p, q, h)
     idx = [0, 1, N // 2, N - 1]
     xs = x[idx].cpu().numpy()
-    cts = nat.words_to_ints(ct[idx].cpu().numpy().view(np.uint32))
+    got = nat.words_to_ints(ct[idx].cpu().numpy().view(np.uint32))
     rs = nat.words_to_ints(rnd[idx].cpu().numpy().view(np.uint32))
     parity_ok = all(O.encrypt_m(okey, O.encode_element(okey, float(xv), 7)[0], rv) == cv
-                    for xv, rv, cv in zip(xs, rs, cts))
+                    for xv, rv, cv in zip(xs, rs, got))
+    if world > 1:  # the reassembled vector holds this rank's shard at its offset
+        parity_ok = parity_ok and bool(torch.equal(gathered[last % nb][rank * N:(rank + 1) * N], ct))
 
     L.xhe_profile(1)
     if world > 1:
@@ -231,7 +268,8 @@ def main():
     t0 = time.time()
     ev0.record()
     for i in range(args.steps):
-        step(i)
+        ct = step(i)
+    drain()
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -256,6 +294,7 @@ def main():
         w_elem, w_pow = algorithmic_macs_per_element(bits, args.win, dk.rand_bits)
         pow_avg_s = (tot.value / max(cnt.value, 1)) / 1e3
         achieved = N * w_pow / pow_avg_s / 1e12  # k_djn_pow: N elements x 2 primes per launch
+        traffic, traffic_src = pmc_traffic(args.win, N)
         rec = {
             "metric": "2048-bit Paillier encrypts/s (device-resident)" if bits == 2048 else f"{bits}-bit Paillier encrypts/s (device-resident)",
             "value": value, "unit": "encrypts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -266,8 +305,8 @@ def main():
                        "key_bits": bits, "elements_per_gpu": N, "fixed_base_window_bits": args.win,
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "valu-int", "achieved": achieved, "peak": PEAK_MAC_PER_S / 1e12,
-                         "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": None,
-                         "kernel": "k_djn_pow", "kernel_avg_ms": pow_avg_s * 1e3,
+                         "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel": "k_djn_pow", "kernel_avg_ms": pow_avg_s * 1e3,
                          "alg_macs_per_element": w_pow},
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,

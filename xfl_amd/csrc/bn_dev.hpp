@@ -31,6 +31,12 @@ namespace xhe {
 #ifndef XHE_MAC_SPLIT
 #define XHE_MAC_SPLIT 1  // a*b mads of a block before its m*N mads
 #endif
+#ifndef XHE_LDS_ROWS
+#define XHE_LDS_ROWS 1  // k_djn_pow_lds: table rows staged in LDS by LDS-DMA bursts
+#endif
+#ifndef XHE_APREF2
+#define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
+#endif
 
 // d = a*b + c with one v_mad_u64_u32. Inline asm keeps a and b 32-bit: the
 // C form (uint64_t)a*b + c makes the compiler hold every limb as a
@@ -533,6 +539,24 @@ struct Mont {
     if constexpr (TPI == 1 && L >= 13) {
       NRes R;
       load_res(Np, R);
+#if XHE_APREF2
+      // operand a two quads ahead (a gathered table row misses L2 often)
+      uint4 nx1 = a.load4(4 < S4 ? 4 : 0);
+      for (; i + 4 <= S; i += 4) {
+        uint4 nx2 = a.load4(i + 8 < S4 ? i + 8 : i);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.x, cur.y, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.y, cur.z, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.z, cur.w, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        step1(Np, R, T, b, cur.w, nx1.x, m, x0, lead);
+        __builtin_amdgcn_sched_barrier(0);
+        cur = nx1;
+        nx1 = nx2;
+      }
+#else
       for (; i + 4 <= S; i += 4) {
         uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
         __builtin_amdgcn_sched_barrier(0);
@@ -546,6 +570,7 @@ struct Mont {
         __builtin_amdgcn_sched_barrier(0);
         cur = nxt;
       }
+#endif
 #pragma unroll
       for (int r = 0; r < (S & 3); ++r)
         step1(Np, R, T, b, comp4(cur, r), r + 1 < (S & 3) ? comp4(cur, r + 1) : 0u, m, x0, lead);

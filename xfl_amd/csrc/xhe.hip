@@ -366,6 +366,13 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     int blocks = (int)((n * MP2::TPI + 255) / 256);
     {
       ProfScope ps("k_djn_pow", s);
+#if XHE_LDS_ROWS
+      if constexpr (MP2::TPI == 1) {
+        hipLaunchKernelGGL(k_djn_pow_lds<MP2>, dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
+                           k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
+                           k->rand_words, n, ws);
+      } else
+#endif
       hipLaunchKernelGGL(k_djn_pow<MP2>, dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
                          m + (size_t)off * k->nw,
                          r + (size_t)off * k->rand_words, k->rand_words, n, ws);

@@ -262,6 +262,59 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
 
+#if XHE_LDS_ROWS
+// Variant of k_djn_pow (TPI == 1) with each product's table row moved into
+// LDS in one burst of LDS-DMA instructions (global_load_lds_dwordx4:
+// instruction k moves quad k of every lane's row; image [quad][lane][4
+// words], read back with conflict-free ds_read_b128). Every 128-B line of a
+// row is then consumed while it is in L2, instead of by 16-B loads spread
+// over the whole product.
+typedef __attribute__((address_space(3))) void xhe_lds_void;
+typedef __attribute__((address_space(1))) void xhe_glb_void;
+struct ALdsQ {
+  const uint32_t* q;  // this lane's slot of the wave image: limb i at q[(i/4)*256 + i%4]
+  XHE_DEV uint4 load4(int i) const { return *reinterpret_cast<const uint4*>(q + (i >> 2) * 256); }
+};
+
+template <class MP2>
+__global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32_t* __restrict__ Np2,
+                                                        const uint32_t* __restrict__ Nq2,
+                                                        const uint32_t* __restrict__ m_words,
+                                                        const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                        uint32_t* __restrict__ ws) {
+  static_assert(MP2::TPI == 1, "LDS row staging is per lane");
+  constexpr int NQ = MP2::S4 / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][NQ * 256];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
+  uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
+  const uint32_t* mine = img + (threadIdx.x & 63) * 4;
+  MP2 M;
+  M.init(prime ? Nq2 : Np2, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{prime ? key.nR2_q2 : key.nR2_p2});  // n m R mod P^2
+  M.add_row(b, md.R1);                              // (1 + n m) R
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  const int rows = 1 << key.win;
+  for (int w = 0; w < key.nwin; ++w) {
+    uint32_t d = digit_at(ae, aw, w * key.win, key.win);
+    const uint32_t* row = tab + ((size_t)w * rows + d) * MP2::S4;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+      __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    M.mul(b, ALdsQ{mine});
+  }
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+}
+#endif
+
 template <class MP2>
 __global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
                                                     uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
