@@ -141,6 +141,18 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream):
     t = _timed(lambda: nat.check(L.xhe_powmod(dk.handle, ct.data_ptr(), k.data_ptr(), 2, 53, nk, ct2.data_ptr(),
                                               stream), "scalar_mul"))
     out["scalar_mul_53bit_per_s"] = nk / t
+    # encrypted mat-vec enc[B] @ X[B, D] at the LR operator's default shape
+    # (logistic_regression/trainer.py:166, B = 2048, D = 15): one
+    # multi-exponentiation with 60-bit exponents (53-bit mantissas + alignment)
+    Bm, Dm = min(N, 2048), 15
+    idx = torch.arange(Bm, dtype=torch.int32, device="cuda").repeat(Dm, 1).contiguous()
+    kx = torch.randint(0, 1 << 30, (Dm, Bm, 2), dtype=torch.int32, device="cuda")
+    kx[..., 1] &= (1 << 28) - 1
+    mv = torch.empty((Dm, dk.n2w), dtype=torch.int32, device="cuda")
+    t = _timed(lambda: nat.check(L.xhe_multiexp(dk.handle, ct.data_ptr(), Bm, idx.data_ptr(), kx.data_ptr(), 2, 60,
+                                                Dm, Bm, 0, mv.data_ptr(), stream), "matvec"))
+    out["matvec_2048x15_s"] = t
+    out["matvec_terms_per_s"] = Bm * Dm / t
     # config 5: 256-bin histogram of 100k ciphertexts (grad) -> segment products
     ns, nb = min(N, 100_000), 256
     seg = (np.arange(nb + 1, dtype=np.int64) * ns) // nb

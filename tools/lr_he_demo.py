@@ -1,0 +1,194 @@
+"""Vertical logistic regression, 2 parties, Paillier — the HE call sequence of
+XFL's demo/vertical/logistic_regression/2party run through the drop-in API
+(BASELINE config 1, with the operator's Paillier config substituted for the
+demo's CKKS block: key 2048, precision 7, DJN on).
+
+Per batch (reference call sites):
+  label trainer  enc = Paillier.encrypt(priv, residual.astype(float32), precision=7,
+                                        obfuscation=True)      label_trainer.py:193-197
+                 bytes = Paillier.serialize(enc)                label_trainer.py:198-200
+  trainer        enc = Paillier.ciphertext_from(pub, bytes)     trainer.py:127
+                 g = np.matmul(enc, x_batch) + noise           trainer.py:162-166
+                 bytes = Paillier.serialize(g)                  trainer.py:168
+  label trainer  dec = Paillier.decrypt(priv, Paillier.ciphertext_from(None, bytes),
+                                        dtype='float')          label_trainer.py:258-259
+  trainer        grad = -(dec - noise) / batch                  trainer.py:176-178
+
+Data: WDBC 569 x 30 (scikit-learn's copy of the UCI file the demo downloads,
+common/dataset/breast_cancer_wisconsin.py:26), z-scored with pandas' std,
+features 0-14 to the label trainer and 15-29 to the trainer, first
+int(569 * 0.3) = 170 rows held out (utils/data_utils.py:104-109), batch 64.
+The models are plain numpy logistic regressions (the HE path does not depend
+on them). `check=True` compares every decrypted gradient bit for bit with the
+plaintext-side restatement of the same homomorphic operations (mod-n
+arithmetic on the encodings, oracle/paillier_oracle.py), independent of the
+obfuscation draws.
+
+    python tools/lr_he_demo.py [--epochs 1] [--check] [--cpu-batches 1]
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def load_wdbc():
+    from sklearn.datasets import load_breast_cancer
+    d = load_breast_cancer()
+    x = d.data.astype(np.float64)
+    x = (x - x.mean(axis=0)) / x.std(axis=0, ddof=1)
+    y = (d.target == 0).astype(np.float32)  # UCI 'M' -> 1 (sklearn encodes malignant as 0)
+    n_test = int(len(x) * 0.3)
+    return x[n_test:].astype(np.float32), y[n_test:], x[:n_test].astype(np.float32), y[:n_test]
+
+
+def sigmoid(z):
+    return 1.0 / (1.0 + np.exp(-z))
+
+
+def expected_noised_gradient(okey, resid32, x32, noise32):
+    """float32 result of decrypt(matmul(encrypt(resid, 7), x) + noise) by
+    mod-n arithmetic on the plaintext encodings (paillier.py:106-187 are exactly
+    homomorphic: c^k -> m k, inv(c)^(n-k) -> m k, c^(2^d) -> m 2^d, c1 c2 -> m1 + m2)."""
+    from oracle import paillier_oracle as O
+    n = okey["n"]
+    enc = [O.encode_element(okey, float(r), 7) for r in resid32]
+    out = []
+    for j in range(x32.shape[1]):
+        am = ae = None
+        for (m, e), xv in zip(enc, x32[:, j]):
+            k, ek = O.encode_scalar(okey, xv.item())
+            pm, pe = (m * k) % n, e + ek
+            if am is None:
+                am, ae = pm, pe
+            else:
+                emin = min(ae, pe)
+                am, ae = ((am << (ae - emin)) + (pm << (pe - emin))) % n, emin
+        km, ke = O.encode_scalar(okey, float(noise32[j]))
+        emin = min(ae, ke)
+        am, ae = ((am << (ae - emin)) + (km << (ke - emin))) % n, emin
+        out.append(O.decode_float32(okey, am, ae))
+    return np.array(out, dtype=np.float32)
+
+
+def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
+    """Runs the HE rounds; returns a dict of phase timings and check results."""
+    from xfl_amd.paillier import Paillier, PaillierContext
+    xtr, ytr, _, _ = load_wdbc()
+    xl, xt = xtr[:, :15], xtr[:, 15:]
+    rng = random.Random(seed)
+    t0 = time.time()
+    priv = key if key is not None else Paillier.context(2048, djn_on=True)
+    pub_bytes = priv.to_public().serialize()
+    pub = Paillier.context_from(pub_bytes)
+    priv.device_key()  # device constants + fixed-base tables, once per key (fit)
+    pub.device_key()
+    t_key = time.time() - t0
+    okey = None
+    if check:
+        from oracle import paillier_oracle as O
+        okey = O.derive_private(priv.p, priv.q, priv.h_pow_n if priv.djn_on else None)
+    wl = np.zeros(15, np.float32)
+    wt = np.zeros(15, np.float32)
+    bias = np.float32(0.0)
+    lr = np.float32(0.01)
+    tm = {"encrypt": 0.0, "serialize": 0.0, "matmul": 0.0, "add_noise": 0.0, "decrypt": 0.0}
+    batches = checked = 0
+    for _ in range(epochs):
+        for s in range(0, len(xtr), batch):
+            if max_batches is not None and batches >= max_batches:
+                break
+            xb_l, xb_t, yb = xl[s:s + batch], xt[s:s + batch], ytr[s:s + batch]
+            pred = sigmoid(xb_l @ wl + xb_t @ wt + bias)
+            resid = (yb - pred).astype(np.float32)  # label side
+            a = time.time()
+            enc = Paillier.encrypt(priv, resid.astype(np.float32).flatten(), precision=7, obfuscation=True)
+            tm["encrypt"] += time.time() - a
+            a = time.time()
+            wire = Paillier.serialize(enc)
+            enc_t = Paillier.ciphertext_from(pub, wire)  # trainer side
+            tm["serialize"] += time.time() - a
+            noise = np.array([rng.randint(1 << 24, 1 << 26) - (1 << 25) for _ in range(xb_t.shape[1])],
+                             dtype=np.float32)
+            noise /= 100000
+            a = time.time()
+            g = np.matmul(enc_t, xb_t)
+            tm["matmul"] += time.time() - a
+            a = time.time()
+            g = g + noise
+            tm["add_noise"] += time.time() - a
+            a = time.time()
+            wire2 = Paillier.serialize(g)
+            tm["serialize"] += time.time() - a
+            a = time.time()
+            dec = Paillier.decrypt(priv, Paillier.ciphertext_from(None, wire2), dtype="float")
+            tm["decrypt"] += time.time() - a
+            if check:
+                want = expected_noised_gradient(okey, resid, xb_t, noise)
+                if not np.array_equal(dec.view(np.uint32), want.view(np.uint32)):
+                    raise AssertionError(f"batch {batches}: decrypted gradient differs from the plaintext restatement")
+                checked += 1
+            gt = np.array(dec, dtype=np.float32) - noise
+            gt = -gt / xb_t.shape[0]
+            gl = -(resid @ xb_l) / xb_l.shape[0]
+            wt -= lr * gt
+            wl -= lr * gl
+            bias -= lr * -np.mean(resid)
+            batches += 1
+    return {"batches": batches, "checked_bit_exact": checked, "key_s": t_key,
+            "phase_s": tm, "he_total_s": sum(tm.values()),
+            "per_batch_ms": {k: 1e3 * v / max(batches, 1) for k, v in tm.items()}}
+
+
+def cpu_batch_seconds(batch=64, seed=0):
+    """The same batch through the reference algorithm restated on the CPU
+    (oracle/paillier_oracle.py, pure-Python pow) — encrypt, matmul fold, noise
+    add, decrypt — for a side-by-side figure. Test/baseline infrastructure."""
+    from oracle import paillier_oracle as O
+    from bench import make_key
+    p, q, n, h = make_key(2048, seed=2024)
+    ok = O.derive_private(p, q, h)
+    xtr, ytr, _, _ = load_wdbc()
+    xb_t = xtr[:batch, 15:]
+    resid = (ytr[:batch] - 0.5).astype(np.float32)
+    rng = random.Random(seed)
+    t = time.time()
+    cts = []
+    for r in resid:
+        m, e = O.encode_element(ok, float(r), 7)
+        cts.append((O.encrypt_m(ok, m, rng.randrange(1, ok["djn_exp_bound"])), e))
+    outs = []
+    for j in range(xb_t.shape[1]):
+        acc = None
+        for (c, e), xv in zip(cts, xb_t[:, j]):
+            tcur = O.mul_ct(ok, c, e, xv.item())
+            acc = tcur if acc is None else O.add_ct(ok, acc[0], acc[1], tcur[0], tcur[1])
+        outs.append(O.add_scalar(ok, acc[0], acc[1], 0.125))
+    for c, e in outs:
+        O.decode_float32(ok, O.decrypt_raw(ok, c), e)
+    return time.time() - t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--cpu-batches", type=int, default=1, help="batches timed through the CPU restatement (0: skip)")
+    args = ap.parse_args()
+    rec = run(epochs=args.epochs, check=args.check)
+    if args.cpu_batches:
+        rec["cpu_restatement_s_per_batch"] = sum(cpu_batch_seconds(seed=i) for i in range(args.cpu_batches)) / \
+            args.cpu_batches
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

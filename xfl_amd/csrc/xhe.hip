@@ -40,11 +40,13 @@ struct HipError : std::runtime_error {
 // Limb shapes per key size: MP2 for residues mod p^2/q^2, MP for mod p/q.
 struct Shape2048 {
   using MP2 = Mont<74, 28, 1>;
+  using MP2L = Mont<76, 28, 4>;  // low-latency (small-batch) decrypt shape
   using MP = Mont<37, 28, 1>;
   using MN2 = Mont<152, 27, 4>;
 };
 struct Shape3072 {
   using MP2 = Mont<110, 28, 2>;
+  using MP2L = Mont<112, 28, 4>;
   using MP = Mont<56, 28, 2>;
   using MN2 = Mont<228, 27, 4>;
 };
@@ -99,11 +101,12 @@ struct xhe_key {
   int K = 0, nw = 0, n2w = 0;
   bool priv = false, djn = false;
   int rand_bits = 0, rand_words = 0;
-  ModSpec mp2{}, mp{}, mn2{};
+  ModSpec mp2{}, mp{}, mn2{}, mp2L{};
   uint32_t* d_blob = nullptr;
   uint32_t* d_tab = nullptr;
   KeyDev kd{};
-  std::vector<uint32_t> n_host;  // n words (for host-side checks)
+  std::vector<uint32_t> n_host;   // n words (for host-side checks)
+  std::vector<uint32_t> n2_host;  // n^2 words (host inverse at the batch-inversion root)
 };
 
 namespace {
@@ -120,29 +123,54 @@ struct DevGuard {
 };
 
 template <class MP2>
-void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s);
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_ws,
+                    hipStream_t s);
 
-template <class Sh>
-void build_tables(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s) {
-  build_tables_m<typename Sh::MP2>(k, md, d_hM, d_tab, s);
+// Tables of one modulus, or of p^2 and q^2 concurrently on two streams.
+template <class MP2>
+void build_tables_sync(xhe_key* k, const ModDev* md, const uint32_t* const* d_hM, uint32_t* const* d_tab, int count) {
+  hipStream_t st[2] = {nullptr, nullptr};
+  uint32_t* ws[2] = {nullptr, nullptr};
+  for (int i = 0; i < count; ++i) {
+    HIPCHK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&ws[i], MP2::S4 * sizeof(uint32_t) * 4));
+    build_tables_m<MP2>(k, md[i], d_hM[i], d_tab[i], ws[i], st[i]);
+  }
+  for (int i = 0; i < count; ++i) {
+    HIPCHK(hipStreamSynchronize(st[i]));
+    HIPCHK(hipFree(ws[i]));
+    HIPCHK(hipStreamDestroy(st[i]));
+  }
 }
 
+// Fixed-base table build, enqueued on `s` (no synchronisation; d_ws must
+// stay alive until s has drained): bases tab[w][1] = h^(2^(win w)) by one
+// squaring chain, every window's low and high chains by doubling levels
+// (k_tab_level: log2 depth instead of 2^(win/2)), then every remaining row
+// as one product of a high and a low entry.
 template <class MP2>
-void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, hipStream_t s) {
-  uint32_t* d_ws = nullptr;
-  HIPCHK(hipMalloc(&d_ws, MP2::S4 * sizeof(uint32_t) * 4));
-  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, k->kd.win, k->kd.nwin, d_tab, d_ws);
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_ws,
+                    hipStream_t s) {
+  const int win = k->kd.win, nwin = k->kd.nwin, half = win / 2;
+  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, win, nwin, d_tab, d_ws);
   HIPCHK(hipGetLastError());
-  int groups_per_block = 64 / MP2::TPI;
-  int blocks = (k->kd.nwin + groups_per_block - 1) / groups_per_block;
-  hipLaunchKernelGGL(k_tab_chain<MP2>, dim3(blocks), dim3(64), 0, s, md, md.N, k->kd.win, k->kd.nwin, d_tab);
+  auto blocks = [&](int64_t groups) { return dim3((unsigned)std::max<int64_t>(1, (groups * MP2::TPI + 255) / 256)); };
+  hipLaunchKernelGGL(k_tab_one<MP2>, blocks(nwin), dim3(256), 0, s, md, win, nwin, d_tab);
   HIPCHK(hipGetLastError());
-  int64_t rows = (int64_t)k->kd.nwin << k->kd.win;
-  int cblocks = (int)((rows * MP2::TPI + 255) / 256);
-  hipLaunchKernelGGL(k_tab_combine<MP2>, dim3(cblocks), dim3(256), 0, s, md, md.N, k->kd.win, k->kd.nwin, d_tab);
+  const int lim_lo = (1 << half) + 1, lim_hi = 1 << (win - half);
+  for (int t = 0; (1 << t) < lim_lo - 1; ++t) {
+    hipLaunchKernelGGL(k_tab_level<MP2>, blocks((int64_t)nwin << t), dim3(256), 0, s, md, md.N, win, nwin, t, 0,
+                       lim_lo, d_tab);
+    HIPCHK(hipGetLastError());
+  }
+  for (int t = 0; (1 << t) < lim_hi - 1; ++t) {
+    hipLaunchKernelGGL(k_tab_level<MP2>, blocks((int64_t)nwin << t), dim3(256), 0, s, md, md.N, win, nwin, t, half,
+                       lim_hi, d_tab);
+    HIPCHK(hipGetLastError());
+  }
+  int64_t rows = (int64_t)nwin << win;
+  hipLaunchKernelGGL(k_tab_combine<MP2>, blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_tab);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipFree(d_ws));
 }
 
 ModDev moddev(uint32_t* base, const ModOff& o) {
@@ -173,7 +201,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   k->rand_words = (k->rand_bits + 31) / 32;
 
   struct {
-    ModOff p2, q2, p, q;
+    ModOff p2, q2, p, q, p2L, q2L;
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
@@ -185,6 +213,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     const ModSpec& s2 = k->mp2;
     const ModSpec& s1 = k->mp;
     o.p2 = put_mod(bl, p2, s2);
+    o.p2L = put_mod(bl, p2, k->mp2L);
+    o.q2L = put_mod(bl, q2, k->mp2L);
     o.q2 = put_mod(bl, q2, s2);
     BigU R2p = pow2((size_t)s2.W * s2.S);
     BigU Rp2 = mod(R2p, p2), Rq2 = mod(R2p, q2);
@@ -254,6 +284,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   kd.n_bits = (int)n.bits();
   if (k->priv) {
     kd.p2 = moddev(B, o.p2);
+    kd.p2L = moddev(B, o.p2L);
+    kd.q2L = moddev(B, o.q2L);
     kd.q2 = moddev(B, o.q2);
     kd.nR2_p2 = B + o.nR2_p2;
     kd.nR2_q2 = B + o.nR2_q2;
@@ -286,16 +318,11 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
       kd.tab_p2 = k->d_tab;
       kd.tab_q2 = k->d_tab + tab_words;
-      hipStream_t s;
-      HIPCHK(hipStreamCreate(&s));
-      if (K == 2048) {
-        build_tables<Shape2048>(k, kd.p2, B + o.hM_p2, k->d_tab, s);
-        build_tables<Shape2048>(k, kd.q2, B + o.hM_q2, k->d_tab + tab_words, s);
-      } else {
-        build_tables<Shape3072>(k, kd.p2, B + o.hM_p2, k->d_tab, s);
-        build_tables<Shape3072>(k, kd.q2, B + o.hM_q2, k->d_tab + tab_words, s);
-      }
-      HIPCHK(hipStreamDestroy(s));
+      const ModDev mds[2] = {kd.p2, kd.q2};
+      const uint32_t* hms[2] = {B + o.hM_p2, B + o.hM_q2};
+      uint32_t* tabs[2] = {k->d_tab, k->d_tab + tab_words};
+      if (K == 2048) build_tables_sync<Shape2048::MP2>(k, mds, hms, tabs, 2);
+      else build_tables_sync<Shape3072::MP2>(k, mds, hms, tabs, 2);
     }
   }
   if (!k->priv && k->djn) {
@@ -305,11 +332,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t tab_words = rows * k->mn2.S4();
     HIPCHK(hipMalloc(&k->d_tab, tab_words * sizeof(uint32_t)));
     kd.tab_n2 = k->d_tab;
-    hipStream_t s;
-    HIPCHK(hipStreamCreate(&s));
-    if (K == 2048) build_tables_m<Shape2048::MN2>(k, kd.n2, B + o_hMn2, k->d_tab, s);
-    else build_tables_m<Shape3072::MN2>(k, kd.n2, B + o_hMn2, k->d_tab, s);
-    HIPCHK(hipStreamDestroy(s));
+    const uint32_t* hm = B + o_hMn2;
+    uint32_t* tab = k->d_tab;
+    if (K == 2048) build_tables_sync<Shape2048::MN2>(k, &kd.n2, &hm, &tab, 1);
+    else build_tables_sync<Shape3072::MN2>(k, &kd.n2, &hm, &tab, 1);
   }
 }
 
@@ -521,7 +547,21 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   uint32_t* y_words = scr + 4 * (k->n2w + 1);
   uint32_t* r_words = y_words + k->n2w;
   hipLaunchKernelGGL(k_row_pack<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, lv + top, r_words);
-  hipLaunchKernelGGL(k_inv_single, dim3(1), dim3(64), 0, s, r_words, k->kd.n2_words, k->n2w, scr, y_words, st);
+  HIPCHK(hipGetLastError());
+  // The one scalar inverse of the batch (the tree root, (prod c_i) R) is a
+  // sequential extended Euclid: ~1 ms on a host core vs a single GPU lane's
+  // tens of milliseconds. Everything per element stays on the device.
+  std::vector<uint32_t> root(k->n2w), yinv(k->n2w);
+  HIPCHK(hipMemcpyAsync(root.data(), r_words, (size_t)k->n2w * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (!modinv_words(root.data(), k->n2_host.data(), k->n2w, yinv.data())) {
+    (void)hipFree(lv);
+    (void)hipFree(inv);
+    (void)hipFree(scr);
+    (void)hipFree(st);
+    return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
+  }
+  HIPCHK(hipMemcpyAsync(y_words, yinv.data(), (size_t)k->n2w * 4, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_inv_to_row<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, y_words, inv + top);
   HIPCHK(hipGetLastError());
   for (size_t l = sizes.size() - 1; l >= 1; --l) {
@@ -531,14 +571,11 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   }
   hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, inv, count, out);
   HIPCHK(hipGetLastError());
-  int32_t hst = 0;
-  HIPCHK(hipMemcpyAsync(&hst, st, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(lv);
   (void)hipFree(inv);
   (void)hipFree(scr);
   (void)hipFree(st);
-  if (hst != 0) return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
   return XHE_OK;
 }
 
@@ -686,13 +723,21 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
   HIPCHK(hipFreeAsync(ws, s));
 }
 
+// Batches up to this size decrypt in the 4-lane shape (latency-bound regime:
+// fewer elements than wave slots x lanes / 2 primes).
+constexpr int64_t kDecLowLatMax = 16384;
+
 template <class Sh>
 void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
   using MP2 = typename Sh::MP2;
+  using MP2L = typename Sh::MP2L;
   using MP = typename Sh::MP;
+  static_assert(MP2L::S4 == MP2::S4, "x rows are shared by both decrypt shapes");
+  const bool lowlat = count <= kDecLowLatMax;
+  const int tpi = lowlat ? MP2L::TPI : MP2::TPI;
   int64_t chunk = std::min<int64_t>(count, kChunk);
-  int pow_blocks = (int)std::min<int64_t>((chunk * MP2::TPI + 255) / 256, 512);
-  int64_t groups = (int64_t)pow_blocks * 256 / MP2::TPI;
+  int pow_blocks = (int)std::min<int64_t>((chunk * tpi + 255) / 256, 512);
+  int64_t groups = (int64_t)pow_blocks * 256 / tpi;
   uint32_t *ws = nullptr, *xrows = nullptr, *mrows = nullptr;
   HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 17 * MP2::S4 * groups * sizeof(uint32_t), s));
   HIPCHK(hipMallocAsync((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
@@ -701,8 +746,12 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
     int64_t n = std::min(chunk, count - off);
     {
       ProfScope ps("k_dec_pow", s);
-      hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
-                         ct + (size_t)off * k->n2w, n, xrows, ws);
+      if (lowlat)
+        hipLaunchKernelGGL((k_dec_pow<MP2L, true>), dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2L.N,
+                           k->kd.q2L.N, ct + (size_t)off * k->n2w, n, xrows, ws);
+      else
+        hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
+                           ct + (size_t)off * k->n2w, n, xrows, ws);
       HIPCHK(hipGetLastError());
     }
     int blocks = (int)((n * MP::TPI + 255) / 256);
@@ -789,10 +838,12 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     k->djn = h_pow_n_words != nullptr;
     if (key_bits == 2048) {
       k->mp2 = {Shape2048::MP2::S, Shape2048::MP2::W};
+      k->mp2L = {Shape2048::MP2L::S, Shape2048::MP2L::W};
       k->mp = {Shape2048::MP::S, Shape2048::MP::W};
       k->mn2 = {Shape2048::MN2::S, Shape2048::MN2::W};
     } else {
       k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
+      k->mp2L = {Shape3072::MP2L::S, Shape3072::MP2L::W};
       k->mp = {Shape3072::MP::S, Shape3072::MP::W};
       k->mn2 = {Shape3072::MN2::S, Shape3072::MN2::W};
     }
@@ -800,6 +851,8 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     if ((int)n.bits() > key_bits || n.bits() + 2 < (size_t)key_bits)
       return fail(XHE_EINVAL, "xhe_key_create: n does not match key_bits");
     k->n_host.assign(n_words, n_words + k->nw);
+    k->n2_host.assign(k->n2w, 0u);
+    mul(n, n).to_words(k->n2_host.data(), k->n2w);
     BigU p, q, h;
     if (k->priv) {
       p = BigU::from_words(p_words, k->nw / 2);

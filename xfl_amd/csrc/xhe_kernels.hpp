@@ -39,6 +39,7 @@ struct KeyDev {
   int ep_bits, eq_bits, n_bits;
   // ---- mod p^2 / q^2 (shape MP2)
   ModDev p2, q2;
+  ModDev p2L, q2L;            // the same moduli in the 4-lane decrypt shape (S = S4 of p2)
   const uint32_t* nR2_p2;     // n * R^2 mod p^2
   const uint32_t* nR2_q2;     // n * R^2 mod q^2
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
@@ -388,13 +389,16 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   }
 }
 
-template <class MP2>
+// LOWLAT: the 4-lane shape (key.p2L/q2L) for small batches, where one lane
+// per residue leaves the chip idle and the 1,280 dependent products of one
+// element set the latency.
+template <class MP2, bool LOWLAT = false>
 __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* __restrict__ Np2,
                                                     const uint32_t* __restrict__ Nq2,
                                                     const uint32_t* __restrict__ c_words, int64_t count,
                                                     uint32_t* __restrict__ xrows, uint32_t* __restrict__ ws) {
   const int prime = blockIdx.y;
-  const ModDev& md = prime ? key.q2 : key.p2;
+  const ModDev& md = LOWLAT ? (prime ? key.q2L : key.p2L) : (prime ? key.q2 : key.p2);
   const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
   const int ebits = prime ? key.qm1_bits : key.pm1_bits;
   const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MP2::TPI;
@@ -811,83 +815,6 @@ __global__ void __launch_bounds__(256, 2) k_tree_down(KeyDev key, const uint32_t
   M.store_strided(b, cinv + i, (int)n_child);
 }
 
-// Single modular inverse x^-1 mod m (binary extended Euclid, one lane), both
-// as nwords little-endian words; m odd. status = 1 when gcd(x, m) != 1.
-__global__ void k_inv_single(const uint32_t* __restrict__ x, const uint32_t* __restrict__ m, int nwords,
-                             uint32_t* __restrict__ scratch, uint32_t* __restrict__ out, int32_t* __restrict__ status) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const int W = nwords + 1;
-  uint32_t *u = scratch, *v = scratch + W, *x1 = scratch + 2 * W, *x2 = scratch + 3 * W;
-  for (int i = 0; i < W; ++i) {
-    u[i] = i < nwords ? x[i] : 0;
-    v[i] = i < nwords ? m[i] : 0;
-    x1[i] = i == 0 ? 1u : 0u;
-    x2[i] = 0;
-  }
-  auto is_one = [&](const uint32_t* a) {
-    if (a[0] != 1) return false;
-    for (int i = 1; i < W; ++i) if (a[i]) return false;
-    return true;
-  };
-  auto is_zero = [&](const uint32_t* a) {
-    for (int i = 0; i < W; ++i) if (a[i]) return false;
-    return true;
-  };
-  auto half = [&](uint32_t* a) {
-    for (int i = 0; i < W; ++i) a[i] = (a[i] >> 1) | (i + 1 < W ? (a[i + 1] << 31) : 0u);
-  };
-  auto add_m_half = [&](uint32_t* a) {  // a = (a + m) / 2  (a < m, so a + m < 2^(32W))
-    uint64_t c = 0;
-    for (int i = 0; i < W; ++i) {
-      c += (uint64_t)a[i] + (i < nwords ? m[i] : 0u);
-      a[i] = (uint32_t)c;
-      c >>= 32;
-    }
-    half(a);
-  };
-  auto geq = [&](const uint32_t* a, const uint32_t* b) {
-    for (int i = W - 1; i >= 0; --i) if (a[i] != b[i]) return a[i] > b[i];
-    return true;
-  };
-  auto sub_to = [&](uint32_t* a, const uint32_t* b) {  // a -= b (a >= b)
-    int64_t br = 0;
-    for (int i = 0; i < W; ++i) {
-      int64_t d = (int64_t)a[i] - b[i] - br;
-      br = d < 0;
-      a[i] = (uint32_t)(d + (br << 32));
-    }
-  };
-  auto submod_to = [&](uint32_t* a, const uint32_t* b) {  // a = (a - b) mod m, a, b < m
-    if (geq(a, b)) { sub_to(a, b); return; }
-    uint64_t c = 0;
-    for (int i = 0; i < W; ++i) {
-      c += (uint64_t)a[i] + (i < nwords ? m[i] : 0u);
-      a[i] = (uint32_t)c;
-      c >>= 32;
-    }
-    sub_to(a, b);
-  };
-  if (is_zero(u)) { status[0] = 1; return; }
-  long guard = 0;
-  while (!is_one(u) && !is_one(v)) {
-    if (++guard > 64L * 32 * W) { status[0] = 1; return; }
-    while ((u[0] & 1) == 0) {
-      half(u);
-      if (x1[0] & 1) add_m_half(x1); else half(x1);
-    }
-    while ((v[0] & 1) == 0) {
-      half(v);
-      if (x2[0] & 1) add_m_half(x2); else half(x2);
-    }
-    if (geq(u, v)) { sub_to(u, v); submod_to(x1, x2); }
-    else { sub_to(v, u); submod_to(x2, x1); }
-    if (is_zero(u) || is_zero(v)) { status[0] = 1; return; }
-  }
-  const uint32_t* r = is_one(u) ? x1 : x2;
-  for (int i = 0; i < nwords; ++i) out[i] = r[i];
-  status[0] = 0;
-}
-
 // n^2 residues (words) -> Montgomery rows [S4][count]; and back.
 template <class MN2>
 __global__ void __launch_bounds__(256, 2) k_to_mont_rows(KeyDev key, const uint32_t* __restrict__ Nn2,
@@ -1056,40 +983,36 @@ __global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* 
   }
 }
 
-// k_tab_chain: one group per window w, half = win/2. With B = tab[w][1]:
-//   tab[w][d]          = B^d            for d < 2^half              (low chain)
-//   tab[w][d << half]  = B^(d << half)  for 0 < d < 2^(win - half)  (high chain)
-// k_tab_combine then fills tab[w][hi|lo] = tab[w][hi] * tab[w][lo].
+// tab[w][0] = R (the digit-0 row: Montgomery one), one group per window
 template <class MP2>
-__global__ void __launch_bounds__(64, 2) k_tab_chain(ModDev md, const uint32_t* __restrict__ Nm, int win, int nwin,
-                                                     uint32_t* __restrict__ tab) {
+__global__ void __launch_bounds__(256, 2) k_tab_one(ModDev md, int win, int nwin, uint32_t* __restrict__ tab) {
   const int w = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI);
   if (w >= nwin) return;
   MP2 M;
-  M.init(Nm, md.n0inv);
-  const int half = win / 2, lo_n = 1 << half, hi_n = 1 << (win - half);
-  uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
+  M.init(md.N, md.n0inv);
   uint32_t b[MP2::L];
   M.load_row(b, md.R1);
   M.reduce_once(b);
-  M.store_row(b, t);  // B^0 = R
-  M.load_row(b, t + MP2::S4);
-  for (int d = 2; d < lo_n; ++d) {
-    M.mul(b, ARow{t + MP2::S4});
-    M.reduce_once(b);
-    M.store_row(b, t + (size_t)d * MP2::S4);
-  }
-  // G = B^(2^half) = B^(2^half - 1) * B
-  M.mul(b, ARow{t + MP2::S4});
+  M.store_row(b, tab + ((size_t)w << win) * MP2::S4);
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_tab_level(ModDev md, const uint32_t* __restrict__ Nm, int win, int nwin,
+                                                       int t, int sh, int lim, uint32_t* __restrict__ tab) {
+  const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  const int64_t per = (int64_t)1 << t;
+  if (idx >= (int64_t)nwin * per) return;
+  const int w = (int)(idx >> t);
+  const int64_t d = per + 1 + (idx & (per - 1));
+  if (d >= lim) return;
+  uint32_t* tw = tab + ((size_t)w << win) * MP2::S4;
+  MP2 M;
+  M.init(Nm, md.n0inv);
+  uint32_t b[MP2::L];
+  M.load_row(b, tw + ((size_t)(d - per) << sh) * MP2::S4);
+  M.mul(b, ARow{tw + ((size_t)per << sh) * MP2::S4});
   M.reduce_once(b);
-  const size_t gs = (size_t)lo_n * MP2::S4;  // row stride of the high chain
-  M.store_row(b, t + gs);
-  wave_sync_mem_();
-  for (int d = 2; d < hi_n; ++d) {
-    M.mul(b, ARow{t + gs});
-    M.reduce_once(b);
-    M.store_row(b, t + (size_t)d * gs);
-  }
+  M.store_row(b, tw + ((size_t)d << sh) * MP2::S4);
 }
 
 template <class MP2>
