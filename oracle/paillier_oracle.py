@@ -295,3 +295,55 @@ def sum_ct(k, raws, exps):
     for c, e in zip(raws, exps):
         acc = acc * pow(c, 1 << (e - emin), n2) % n2
     return acc, emin
+
+
+# ------------------------------------------------------------------ packing
+def embed_ref(p_list, interval=1 << 128, precision=64):
+    """algorithm/core/paillier_acceleration.py:21-32, element by element."""
+    out = []
+    for i in range(len(p_list[0])):
+        x = int(p_list[0][i] * (1 << precision))
+        for j in range(len(p_list) - 1):
+            x = x * interval + int(p_list[j + 1][i] * (1 << precision))
+        out.append(x)
+    return out
+
+
+def umbed_ref(a, num, interval=1 << 128, precison=64):
+    """algorithm/core/paillier_acceleration.py:35-59 -> num lists of float32."""
+    import numpy as np
+    out = [[0] * len(a) for _ in range(num)]
+    for i, x in enumerate(a):
+        res = [0] * num
+        b = x % interval
+        if abs(b) > interval // 2:
+            b = b - interval
+        a2 = (x - b) // interval
+        res[-1] = b / (1 << precison)
+        for k in range(num - 1):
+            b = a2 % interval
+            if abs(b) > interval // 2:
+                b = b - interval
+            a2 = (a2 - b) // interval
+            res[-k - 2] = b / (1 << precison)
+        t = np.array(res).astype(np.float32)
+        for j in range(num):
+            out[j][i] = t[j]
+    return out
+
+
+def unpack_ref(x, num, interval=1 << 128, precison=64):
+    """algorithm/core/paillier_acceleration.py:62-81."""
+    res = [0] * num
+    b = x % interval
+    if abs(b) > interval // 2:
+        b = b - interval
+    a = (x - b) // interval
+    res[-1] = float(b / (1 << precison))
+    for i in range(num - 1):
+        b = a % interval
+        if abs(b) > interval // 2:
+            b = b - interval
+        a = (a - b) // interval
+        res[-i - 2] = float(b / (1 << precison))
+    return res
