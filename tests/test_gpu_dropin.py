@@ -195,3 +195,42 @@ def test_rest_errors_and_djn():
         Paillier.decrypt(djn, 123)
     with pytest.raises(TypeError):
         Paillier.obfuscate(123)
+
+
+def test_deferred_sums_groupby_and_chains():
+    """pandas groupby sum / np.sum / sum() over object columns build deferred
+    sums (one segmented-product call when read); results equal the oracle's
+    aligned product, including mixed exponents and shared operands."""
+    import time
+
+    import pandas as pd
+
+    from oracle import paillier_oracle as O
+    from xfl_amd.paillier import PaillierCiphertext
+    g = load_fixture(FIXTURES[0])
+    priv, pub = _ctxs(g)
+    k = g["key"]
+    ok = O.derive_private(hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"]))
+    rng = random.Random(9)
+    n2 = ok["n_square"]
+    N, NB = 3000, 32
+    raws = [rng.randrange(2, n2) for _ in range(N)]
+    exps = [rng.choice([0, -3, -7]) for _ in range(N)]
+    bins = [rng.randrange(NB) for _ in range(N)]
+    cts = [PaillierCiphertext(pub, r, e) for r, e in zip(raws, exps)]
+    t = time.time()
+    df = pd.DataFrame({"bin": bins, "c": np.array(cts, dtype=object)})
+    agg = df.groupby(["bin"])["c"].agg(["count", "sum"])
+    got = [(c.raw_ciphertext, c.exponent) for c in agg["sum"]]
+    elapsed = time.time() - t
+    for b in range(NB):
+        idx = [i for i in range(N) if bins[i] == b]
+        assert got[b] == O.sum_ct(ok, [raws[i] for i in idx], [exps[i] for i in idx])
+    assert elapsed < 30, f"groupby over {N} ciphertexts took {elapsed:.1f}s"
+    # a chain reusing one operand, then an eager op on the deferred result
+    s = cts[0] + cts[1]
+    s2 = s + cts[0] + s
+    want = O.sum_ct(ok, [raws[0], raws[1], raws[0], raws[0], raws[1]], [exps[0], exps[1], exps[0], exps[0], exps[1]])
+    assert (s2.raw_ciphertext, s2.exponent) == want
+    m = s2 * 3
+    assert m.raw_ciphertext == O.mul_ct(ok, want[0], want[1], 3)[0]

@@ -25,6 +25,11 @@ def _ct_type():
     return PaillierCiphertext
 
 
+def _raws(cts):
+    from .paillier import raws_of
+    return raws_of(cts)
+
+
 class PaillierArray(np.ndarray):
     def __new__(cls, obj):
         return np.asarray(obj, dtype=object).view(cls)
@@ -62,7 +67,7 @@ class PaillierArray(np.ndarray):
             if flat.size >= 2 and all(isinstance(c, CT) for c in flat):
                 _check_same_key(list(flat))
                 ctx = flat[0].context
-                r, e = ops.segment_sums(ctx, [c.raw_ciphertext for c in flat], [c.exponent for c in flat],
+                r, e = ops.segment_sums(ctx, _raws(list(flat)), [c.exponent for c in flat],
                                         [0, flat.size])
                 return CT(ctx, r[0], int(e[0]))
         return _wrap(np.ndarray.sum(np.asarray(self).view(np.ndarray), axis=axis, dtype=dtype, out=out,
@@ -119,8 +124,8 @@ def _add(a, b):
     if pairs:
         _check_same_key([p[1] for p in pairs] + [p[2] for p in pairs])
         ctx = pairs[0][1].context
-        r, e = ops.add(ctx, [p[1].raw_ciphertext for p in pairs], [p[1].exponent for p in pairs],
-                       [p[2].raw_ciphertext for p in pairs], [p[2].exponent for p in pairs])
+        r, e = ops.add(ctx, _raws([p[1] for p in pairs]), [p[1].exponent for p in pairs],
+                       _raws([p[2] for p in pairs]), [p[2].exponent for p in pairs])
         for (i, x, _), rv, ev in zip(pairs, r, e):
             out[i] = CT(x.context, rv, int(ev))
     if scal:
@@ -128,7 +133,7 @@ def _add(a, b):
         ctx = scal[0][1].context
         enc = Paillier.encrypt(ctx, np.array([s for _, _, s in scal], dtype=object), precision=None,
                                max_exponent=None, obfuscation=False)
-        r, e = ops.add(ctx, [c.raw_ciphertext for _, c, _ in scal], [c.exponent for _, c, _ in scal],
+        r, e = ops.add(ctx, _raws([c for _, c, _ in scal]), [c.exponent for _, c, _ in scal],
                        [c.raw_ciphertext for c in enc], [c.exponent for c in enc])
         for (i, c, _), rv, ev in zip(scal, r, e):
             out[i] = CT(c.context, rv, int(ev))
@@ -161,7 +166,7 @@ def _mul(a, b):
             e = PaillierEncoder.cal_exponent(s, precision=None)
             ks.append(int(PaillierEncoder.encode_single(c.context, s, e)))
             es.append(int(e))
-        r = ops.raw_mul(ctx, [c.raw_ciphertext for _, c, _ in items], ks)
+        r = ops.raw_mul(ctx, _raws([c for _, c, _ in items]), ks)
         for (i, c, _), rv, ev in zip(items, r, es):
             out[i] = CT(c.context, rv, ev + c.exponent)
     return out.reshape(shape).view(PaillierArray)
@@ -223,10 +228,10 @@ def _matmul(a, b):
     emin = ex.min(axis=0)
     need_inv = [i for i in range(Bn) if any(neg[i])]
     # bases: the B ciphertexts, then the inverses of those with a negative scalar
-    bases = [A[i].raw_ciphertext for i in range(Bn)]
+    bases = _raws(list(A))
     inv_slot = {}
     if need_inv:
-        r = ops.powmod(ctx, [A[i].raw_ciphertext for i in need_inv], [1] * len(need_inv), invert_first=True)
+        r = ops.powmod(ctx, [bases[i] for i in need_inv], [1] * len(need_inv), invert_first=True)
         for i, v in zip(need_inv, r):
             inv_slot[i] = len(bases)
             bases.append(v)

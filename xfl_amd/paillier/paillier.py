@@ -36,12 +36,37 @@ def _is_scalar(x):
 
 
 class PaillierCiphertext(object):
-    """paillier.py:45-232"""
+    """paillier.py:45-232
+
+    Ciphertext + ciphertext is DEFERRED: the result records its two operands
+    and its exponent (min of theirs, paillier.py:106-123) and computes the
+    residue on first use. The folded value of any tree of such additions is
+    prod c_i^(2^(e_i - e_min)) mod n^2 in any order, so a
+    chain of n additions (pandas groupby sum, np.sum over object arrays,
+    Python sum()) costs n O(1) Python steps and ONE segmented-product kernel
+    call when the result is read, instead of n device round trips. Reading
+    raw_ciphertext, serializing, decrypting or any batched operation
+    materializes (materialize() does a whole array in one call).
+    """
 
     def __init__(self, context: PaillierContext, raw_ciphertext: MPZ, exponent: int) -> None:
         self.__context = context
-        self.__c = int(raw_ciphertext)
+        self.__c = None if raw_ciphertext is None else int(raw_ciphertext)
         self.__exp = int(exponent)
+        self._parts = None  # (a, b) while this is a deferred a + b
+
+    @classmethod
+    def _deferred_sum(cls, a, b):
+        ct = cls(a.context, None, min(a.exponent, b.exponent))
+        ct._parts = (a, b)
+        return ct
+
+    def _is_deferred(self):
+        return self.__c is None
+
+    def _set_raw(self, raw):
+        self.__c = int(raw)
+        self._parts = None
 
     @property
     def context(self):
@@ -49,6 +74,8 @@ class PaillierCiphertext(object):
 
     @property
     def raw_ciphertext(self):
+        if self.__c is None:
+            materialize([self])
         return self.__c
 
     @property
@@ -57,7 +84,7 @@ class PaillierCiphertext(object):
 
     def serialize(self, compression: bool = True) -> bytes:
         from ..compat import compress, dumps
-        out = dumps(RawCiphertext(self.__c, self.__exp))
+        out = dumps(RawCiphertext(self.raw_ciphertext, self.__exp))
         return compress(out) if compression else out
 
     @classmethod
@@ -71,7 +98,7 @@ class PaillierCiphertext(object):
     def _decrease_exponent_to(self, new_exponent: int):
         """paillier.py:79-86"""
         scalar = 1 << (self.__exp - new_exponent)
-        return ops.raw_mul(self.__context, [self.__c], [scalar])[0]
+        return ops.raw_mul(self.__context, [self.raw_ciphertext], [scalar])[0]
 
     def __add__(self, other):
         """paillier.py:88-104 (no obfuscation when adding a scalar)."""
@@ -84,11 +111,10 @@ class PaillierCiphertext(object):
             raise TypeError(f"Adding data of type {type(other)} not supported.")
 
     def _add_encrypted(self, other):
-        """paillier.py:106-123"""
-        if self.context.to_public() != other.context.to_public():
+        """paillier.py:106-123 (deferred: see the class docstring)"""
+        if self.context is not other.context and self.context.to_public() != other.context.to_public():
             raise ValueError("Adding two ciphertext with different keys.")
-        r, e = ops.add(self.context, [self.__c], [self.__exp], [other.raw_ciphertext], [other.exponent])
-        return PaillierCiphertext(self.context, r[0], int(e[0]))
+        return PaillierCiphertext._deferred_sum(self, other)
 
     def __radd__(self, other):
         return self.__add__(other)
@@ -105,7 +131,7 @@ class PaillierCiphertext(object):
             raise TypeError("Cannot multiply one ciphertext with another ciphertext, try multiply a scalar.")
         exponent = PaillierEncoder.cal_exponent(scalar, precision=None)
         encoded_scalar = PaillierEncoder.encode_single(self.context, scalar, exponent)
-        raw = ops.raw_mul(self.__context, [self.__c], [encoded_scalar])[0]
+        raw = ops.raw_mul(self.__context, [self.raw_ciphertext], [encoded_scalar])[0]
         return PaillierCiphertext(self.context, raw, exponent + self.exponent)
 
     def __rmul__(self, scalar: Union[int, float]):
@@ -116,8 +142,45 @@ class PaillierCiphertext(object):
 
     def obfuscate(self):
         """paillier.py:189-232 (fresh device-drawn a / r)."""
-        self.__c = ops.obfuscate(self.__context, [self.__c])[0]
+        self._set_raw(ops.obfuscate(self.__context, [self.raw_ciphertext])[0])
         return self
+
+
+def materialize(cts):
+    """Compute every deferred sum among `cts` with one segmented product per
+    key: each deferred ciphertext becomes the product of the leaves of its
+    addition tree, aligned to its exponent (paillier.py:79-86,106-123)."""
+    pending = [c for c in cts if isinstance(c, PaillierCiphertext) and c._is_deferred()]
+    if not pending:
+        return
+    by_ctx = {}
+    seen = set()
+    for c in pending:
+        if id(c) not in seen:
+            seen.add(id(c))
+            by_ctx.setdefault(id(c.context), []).append(c)
+    for group in by_ctx.values():
+        raws, exps, seg = [], [], [0]
+        for root in group:
+            stack = [root]
+            while stack:  # iterative: addition chains can be 10^5 deep
+                node = stack.pop()
+                if node._is_deferred():
+                    stack.extend(node._parts)
+                else:
+                    raws.append(node.raw_ciphertext)
+                    exps.append(node.exponent)
+            seg.append(len(raws))
+        r, e = ops.segment_sums(group[0].context, raws, exps, seg)
+        for root, rv, ev in zip(group, r, e):
+            assert int(ev) == root.exponent
+            root._set_raw(rv)
+
+
+def raws_of(cts):
+    """raw ciphertexts of a sequence, deferred sums materialized in one batch"""
+    materialize(cts)
+    return [c.raw_ciphertext for c in cts]
 
 
 def _to_ciphertexts(context, raws, exps, shape):
@@ -157,6 +220,9 @@ class Paillier(object):
         from ..compat import compress, dumps
         if isinstance(data, PaillierCiphertext):
             return data.serialize(compression)
+
+        if isinstance(data, np.ndarray) and data.dtype == object:
+            materialize(list(data.reshape(-1)))
 
         def f(x):
             return RawCiphertext(x.raw_ciphertext, x.exponent)
@@ -254,13 +320,13 @@ class Paillier(object):
             flat = data.reshape(-1)
             idx = [i for i, x in enumerate(flat) if isinstance(x, PaillierCiphertext)]
             if not out_origin and dtype == 'float' and len(idx) == len(flat) and len(flat) > 0:
-                _, f32, st = ops.decrypt_float32(context, [x.raw_ciphertext for x in flat],
+                _, f32, st = ops.decrypt_float32(context, raws_of(list(flat)),
                                                  [x.exponent for x in flat])
                 if np.any(st != 0):
                     raise OverflowError("Overflow detected during decoding encrypted number.")
                 return f32.reshape(shape)
             vals = list(flat)
-            ms = ops.decrypt_ints(context, [flat[i].raw_ciphertext for i in idx])
+            ms = ops.decrypt_ints(context, raws_of([flat[i] for i in idx]))
             for i, m in zip(idx, ms):
                 vals[i] = PaillierEncoder.decode_single(context, m, flat[i].exponent)
             out = np.empty(len(vals), dtype=object)
@@ -299,7 +365,7 @@ class Paillier(object):
                 raise TypeError("Unsupported raw ciphertext type")
             if len(flat):
                 ctx = flat[0].context
-                raws = ops.obfuscate(ctx, [c.raw_ciphertext for c in flat])
+                raws = ops.obfuscate(ctx, raws_of(list(flat)))
                 out = np.empty(len(flat), dtype=object)
                 for i, (c, r) in enumerate(zip(flat, raws)):
                     out[i] = PaillierCiphertext(c.context, r, c.exponent)
