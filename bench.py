@@ -110,7 +110,7 @@ def _timed(fn, reps=3):
     return (time.time() - t0) / reps
 
 
-def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream):
+def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
     """Rates of the other operations on the path (BASELINE configs 2, 3, 5),
     device-resident except where named; plus the host-buffer (PCIe-inclusive)
     encrypt/decrypt rates. Each is checked where a cheap property exists."""
@@ -166,8 +166,26 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream):
     t = _timed(lambda: nat.check(L.xhe_segprod(dk.handle, ct.data_ptr(), None, 0, N, one.ctypes.data_as(
         ctypes.c_void_p), 1, hist.data_ptr(), stream), "sum"), reps=2)
     out["sum_per_s"] = N / t
+    # the other encryption modes: a remote party holding only
+    # the public key (DJN is lost on the wire, context.py:152-168, so it runs
+    # r^n mod n^2 with a variable base: paillier.py:228-230), the public DJN
+    # form (fixed base mod n^2, paillier.py:210-212) and the private non-DJN
+    # CRT form (paillier.py:214-227)
+    p_, q_, n_, h_ = key_material
+    nm = min(N, 1 << 16)
+    rk = torch.empty((nm, dk.nw), dtype=torch.int32, device="cuda")
+    ctm = torch.empty((nm, dk.n2w), dtype=torch.int32, device="cuda")
+    for tag, args_ in (("encrypt_public_nodjn_per_s", (None, None, None)),
+                       ("encrypt_public_djn_per_s", (None, None, h_)),
+                       ("encrypt_private_nodjn_per_s", (p_, q_, None))):
+        k2 = nat.DeviceKey(dk.key_bits, n_, *args_, device=dk.device, win_bits=8 if args_[2] else 0)
+        nat.check(L.xhe_rand(k2.handle, b"\x01" * 32, 5, nm, rk.data_ptr(), None, stream), "rand")
+        t = _timed(lambda: nat.check(L.xhe_encrypt(k2.handle, m.data_ptr(), rk.data_ptr(), nm, ctm.data_ptr(), stream),
+                                     tag), reps=2)
+        out[tag] = nm / t
+        del k2
     # host buffers in and out (PCIe-inclusive), the rate the federated exchange sees
-    nh = min(N, 1 << 18)
+    nh = min(N, 1 << 20)
     xh = x[:nh].cpu().numpy()
     cth = np.empty((nh, dk.n2w), dtype=np.uint32)
     exh = np.empty(nh, dtype=np.int32)
@@ -324,7 +342,7 @@ def main():
             "key_setup_s": t_key,
         }
         if not args.no_ops:
-            rec["ops"] = measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream)
+            rec["ops"] = measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, (p, q, n, h))
         if not args.no_cpu_baseline:
             cores = min(os.cpu_count() or 1, 16)
             rec["cpu_baseline"] = cpu_baseline(bits, args.cpu_seconds, cores)

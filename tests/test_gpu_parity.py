@@ -57,3 +57,44 @@ def test_decrypt_bit_exact(fx, case):
     cw = ints_to_words([hx(r) for r in enc["raw"]], dk.n2w)
     out = words_to_ints(dk.decrypt_words(cw))
     assert out == [hx(m) for m in ms]
+
+
+def test_host_encrypt_chunking_is_invisible():
+    """xhe_encrypt_f64_host pipelines 64k-element chunks over two streams; the
+    randomness is drawn at global element positions, so the result equals one
+    device-resident encode + draw + encrypt of the whole batch, and spot
+    elements equal the oracle's encryption with the drawn a."""
+    import ctypes
+
+    import torch
+
+    from xfl_amd import _native as nat
+    g = load_fixture(FIXTURES[0])
+    dk = _dkey(g)
+    ok = _okey(g)
+    L = nat.lib()
+    n = 200_003
+    x = np.random.default_rng(3).standard_normal(n)
+    seed, nonce = bytes(range(32)), 77
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    ct = np.empty((n, dk.n2w), np.uint32)
+    ex = np.empty(n, np.int32)
+    st = np.empty(n, np.int32)
+    nat.check(L.xhe_encrypt_f64_host(dk.handle, vp(x), n, 7, 0, 0, 1, seed, nonce, vp(ct), vp(ex), vp(st)), "host")
+    xd = torch.from_numpy(x).cuda()
+    m = torch.empty((n, dk.nw), dtype=torch.int32, device="cuda")
+    e = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.empty(n, dtype=torch.int32, device="cuda")
+    r = torch.empty((n, dk.rand_words), dtype=torch.int32, device="cuda")
+    c = torch.empty((n, dk.n2w), dtype=torch.int32, device="cuda")
+    strm = torch.cuda.current_stream().cuda_stream
+    nat.check(L.xhe_encode_f64(dk.handle, xd.data_ptr(), n, 7, 0, 0, m.data_ptr(), e.data_ptr(), s.data_ptr(), strm))
+    nat.check(L.xhe_rand(dk.handle, seed, nonce, n, r.data_ptr(), None, strm))
+    nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), r.data_ptr(), n, c.data_ptr(), strm))
+    torch.cuda.synchronize()
+    assert np.array_equal(c.cpu().numpy().view(np.uint32), ct)
+    assert np.array_equal(e.cpu().numpy(), ex) and not st.any()
+    for i in (0, 65535, 65536, 131072, n - 1):
+        mi = O.encode_element(ok, float(x[i]), 7)[0]
+        ai = nat.words_to_ints(r[i].cpu().numpy().view(np.uint32))
+        assert nat.words_to_ints(ct[i]) == O.encrypt_m(ok, mi, ai)

@@ -813,6 +813,21 @@ struct Stream {
 };
 }  // namespace
 
+namespace {
+// Draws for elements [base, base + count) of the stream (seed32, nonce).
+void rand_impl(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_t base, int64_t count,
+               uint32_t* rand_dev, int32_t* status_dev, hipStream_t s) {
+  ChaChaKey ck;
+  memcpy(ck.k, seed32, 32);
+  ck.nonce0 = (uint32_t)nonce;
+  ck.nonce1 = (uint32_t)(nonce >> 32);
+  int blocks = (int)((count + 255) / 256);
+  hipLaunchKernelGGL(k_rand_below, dim3(blocks), dim3(256), 0, s, ck, base, count, key->rand_words, key->rand_bits,
+                     key->djn ? (const uint32_t*)nullptr : key->kd.n_words, rand_dev, status_dev);
+  HIPCHK(hipGetLastError());
+}
+}  // namespace
+
 extern "C" {
 
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
@@ -915,14 +930,7 @@ int xhe_rand(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_t 
     if (!key || !seed32 || (count > 0 && !rand_dev)) return fail(XHE_EINVAL, "xhe_rand: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    ChaChaKey ck;
-    memcpy(ck.k, seed32, 32);
-    ck.nonce0 = (uint32_t)nonce;
-    ck.nonce1 = (uint32_t)(nonce >> 32);
-    int blocks = (int)((count + 255) / 256);
-    hipLaunchKernelGGL(k_rand_below, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ck, count, key->rand_words,
-                       key->rand_bits, key->djn ? (const uint32_t*)nullptr : key->kd.n_words, rand_dev, status_dev);
-    HIPCHK(hipGetLastError());
+    rand_impl(key, seed32, nonce, 0, count, rand_dev, status_dev, (hipStream_t)stream);
     return XHE_OK;
   });
 }
@@ -1067,23 +1075,47 @@ int xhe_encrypt_f64_host(const xhe_key* key, const double* x, int64_t count, int
       return fail(XHE_EINVAL, "xhe_encrypt_f64_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    Stream st;
-    DevBuf dx(count * 8, st.s), dm((size_t)count * key->nw * 4, st.s), de(count * 4, st.s), ds(count * 4, st.s),
-        dc((size_t)count * key->n2w * 4, st.s), dr(obfuscate ? (size_t)count * key->rand_words * 4 : 4, st.s);
-    HIPCHK(hipMemcpyAsync(dx.p, x, count * 8, hipMemcpyHostToDevice, st.s));
-    int rc = xhe_encode_f64(key, dx.as<double>(), count, precision, has_max, max_exponent, dm.as<uint32_t>(),
-                            de.as<int32_t>(), ds.as<int32_t>(), st.s);
-    if (rc != XHE_OK) return rc;
-    if (obfuscate) {
-      rc = xhe_rand(key, seed32, nonce, count, dr.as<uint32_t>(), nullptr, st.s);
-      if (rc != XHE_OK) return rc;
+    // Chunks alternate between two streams: chunk i+1's upload and kernels are
+    // enqueued before chunk i's (host-blocking, pageable) download, so the
+    // PCIe copy-out of one chunk overlaps the kernels of the next. The
+    // randomness is drawn at global element positions, so the ciphertexts do
+    // not depend on the chunking.
+    const int64_t chunk = count >= (1 << 17) ? (1 << 16) : count;
+    const int64_t nch = (count + chunk - 1) / chunk;
+    Stream st[2];
+    std::unique_ptr<DevBuf> dx[2], dm[2], de[2], ds[2], dc[2], dr[2];
+    for (int b = 0; b < (nch > 1 ? 2 : 1); ++b) {
+      dx[b].reset(new DevBuf(chunk * 8, st[b].s));
+      dm[b].reset(new DevBuf((size_t)chunk * key->nw * 4, st[b].s));
+      de[b].reset(new DevBuf(chunk * 4, st[b].s));
+      ds[b].reset(new DevBuf(chunk * 4, st[b].s));
+      dc[b].reset(new DevBuf((size_t)chunk * key->n2w * 4, st[b].s));
+      dr[b].reset(new DevBuf(obfuscate ? (size_t)chunk * key->rand_words * 4 : 4, st[b].s));
     }
-    rc = xhe_encrypt(key, dm.as<uint32_t>(), obfuscate ? dr.as<uint32_t>() : nullptr, count, dc.as<uint32_t>(), st.s);
+    auto enqueue = [&](int64_t c) -> int {
+      const int b = (int)(c & 1);
+      const int64_t off = c * chunk, n = std::min(chunk, count - off);
+      hipStream_t s = st[b].s;
+      HIPCHK(hipMemcpyAsync(dx[b]->p, x + off, n * 8, hipMemcpyHostToDevice, s));
+      int rc = xhe_encode_f64(key, dx[b]->as<double>(), n, precision, has_max, max_exponent, dm[b]->as<uint32_t>(),
+                              de[b]->as<int32_t>(), ds[b]->as<int32_t>(), s);
+      if (rc != XHE_OK) return rc;
+      if (obfuscate) rand_impl(key, seed32, nonce, off, n, dr[b]->as<uint32_t>(), nullptr, s);
+      return xhe_encrypt(key, dm[b]->as<uint32_t>(), obfuscate ? dr[b]->as<uint32_t>() : nullptr, n,
+                         dc[b]->as<uint32_t>(), s);
+    };
+    int rc = enqueue(0);
     if (rc != XHE_OK) return rc;
-    HIPCHK(hipMemcpyAsync(ct, dc.p, (size_t)count * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipMemcpyAsync(exps, de.p, count * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipMemcpyAsync(status, ds.p, count * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipStreamSynchronize(st.s));
+    for (int64_t c = 0; c < nch; ++c) {
+      if (c + 1 < nch && (rc = enqueue(c + 1)) != XHE_OK) return rc;
+      const int b = (int)(c & 1);
+      const int64_t off = c * chunk, n = std::min(chunk, count - off);
+      hipStream_t s = st[b].s;
+      HIPCHK(hipMemcpyAsync(ct + (size_t)off * key->n2w, dc[b]->p, (size_t)n * key->n2w * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(exps + off, de[b]->p, n * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(status + off, ds[b]->p, n * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));  // chunk c+2 reuses buffer b
+    }
     return XHE_OK;
   });
 }

@@ -173,13 +173,16 @@ struct ChaChaKey { uint32_t k[8]; uint32_t nonce0, nonce1; };
 
 // Uniform integers in [1, 2^bits) (DJN a, paillier.py:195) when bound == null,
 // else in [1, bound) by rejection (non-DJN r in [1, n), paillier.py:215).
-// `words` 32-bit words per element; element i uses counter block
-// (i * 16 + attempt) * blocks_per_draw.
-__global__ void k_rand_below(ChaChaKey ck, int64_t count, int words, int bits, const uint32_t* __restrict__ bound,
-                             uint32_t* __restrict__ out, int32_t* __restrict__ status) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  uint32_t* o = out + (size_t)i * words;
+// `words` 32-bit words per element; element i (= base + thread) uses counter
+// block (i * 64 + attempt) * blocks_per_draw.
+__global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
+                             const uint32_t* __restrict__ bound, uint32_t* __restrict__ out,
+                             int32_t* __restrict__ status) {
+  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= count) return;
+  uint32_t* o = out + (size_t)li * words;
+  status = status ? status + li : nullptr;
+  const int64_t i = base + li;  // stream position: independent of how a batch is split into launches
   const int blocks = (words + 15) / 16;
   for (int attempt = 0; attempt < 64; ++attempt) {
     for (int b = 0; b < blocks; ++b) {
@@ -201,9 +204,9 @@ __global__ void k_rand_below(ChaChaKey ck, int64_t count, int words, int bits, c
       for (int k = words - 1; k >= 0 && c == 0; --k) c = o[k] < bound[k] ? -1 : (o[k] > bound[k] ? 1 : 0);
       ok = c < 0;
     }
-    if (ok) { if (status) status[i] = ST_OK; return; }
+    if (ok) { if (status) *status = ST_OK; return; }
   }
-  if (status) status[i] = ST_VALUE;
+  if (status) *status = ST_VALUE;
 }
 
 // ============================================================== encrypt
