@@ -96,3 +96,20 @@ def test_device_key_bits():
     assert device_key_bits((1 << 3071) + 1) == 3072
     with pytest.raises(NotImplementedError):
         device_key_bits(15)
+
+
+def test_utils_scalar_helpers_match_reference_formulas(golden):
+    """utils.py:38-76 scalar helpers (API completeness) on the fixture key."""
+    from xfl_amd.paillier import utils as U
+    k = golden["key"]
+    p, q = hx(k["p"]), hx(k["q"])
+    n = p * q
+    qi = pow(q, -1, p)
+    for x in (0, 1, 12345, n - 1, n // 3):
+        assert U.crt(x % p, x % q, p, q, qi, n) == x
+    assert U.mulmod(n - 1, n - 2, n) == 2
+    assert U.powmod(1, n, 7) == 1 and U.powmod(3, 5, 7) == 5
+    assert U.invert(3, 7) == 5
+    import pytest
+    with pytest.raises(ZeroDivisionError):
+        U.invert(p, n)

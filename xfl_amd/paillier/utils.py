@@ -24,6 +24,26 @@ def mul(a, b):
     return a * b
 
 
+# Scalar helpers kept for API completeness (utils.py:38-68); the batched
+# device path never calls them.
+def crt(mp, mq, p, q, q_inverse, n):
+    """utils.py:38-43"""
+    u = ((mp - mq) * q_inverse) % p
+    return int((mq + u * q) % n)
+
+
+def mulmod(a, b, c):
+    """utils.py:50-54"""
+    return (a * b) % c
+
+
+def powmod(a: int, b: int, c: int) -> int:
+    """utils.py:57-68 (powmod(1, ., .) = 1 as in the reference)"""
+    if a == 1:
+        return 1
+    return pow(a, b, c)
+
+
 def invert(a, b):
     """utils.py:71-76: ZeroDivisionError when no inverse exists."""
     try:
