@@ -9,6 +9,17 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# One HIP runtime per process: torch ships its own libamdhip64, and if
+# libxhe.so (linked against the system ROCm) initialises the runtime first, a
+# later torch.cuda call in the same process finds "No HIP GPUs". Initialising
+# torch first makes libxhe bind to the runtime torch loaded (as bench.py does).
+try:
+    import torch as _torch
+    if _torch.cuda.is_available():
+        _torch.cuda.init()
+except Exception:  # no torch / no GPU: CPU-only runs
+    pass
 FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json"]
 
 

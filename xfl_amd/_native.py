@@ -82,6 +82,14 @@ def lib():
             if not os.path.exists(LIB_PATH):
                 raise XheError(f"xfl_amd native library not built: {LIB_PATH} missing "
                                "(run __graft_entry__.build())")
+            # One HIP runtime per process: PyTorch-ROCm bundles its own
+            # libamdhip64. Loading torch first makes libxhe bind to that copy;
+            # the other order leaves torch.cuda with "No HIP GPUs" later in
+            # the same process (XFL's operators import torch anyway).
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)

@@ -280,28 +280,20 @@ struct ALdsQ {
   XHE_DEV uint4 load4(int i) const { return *reinterpret_cast<const uint4*>(q + (i >> 2) * 256); }
 };
 
+// c_P = (1 + n m) h^a mod P^2 for one element and one prime, table rows
+// through the wave's LDS image; written as row `prime` of ws.
 template <class MP2>
-__global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32_t* __restrict__ Np2,
-                                                        const uint32_t* __restrict__ Nq2,
-                                                        const uint32_t* __restrict__ m_words,
-                                                        const uint32_t* __restrict__ a_words, int aw, int64_t count,
-                                                        uint32_t* __restrict__ ws) {
-  static_assert(MP2::TPI == 1, "LDS row staging is per lane");
+XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, const ModDev& md,
+                           const uint32_t* tab, const uint32_t* nR2, const uint32_t* __restrict__ m_words,
+                           const uint32_t* __restrict__ a_words, int aw, int64_t count, int64_t e, int prime,
+                           uint32_t* img, const uint32_t* mine, uint32_t* __restrict__ ws) {
   constexpr int NQ = MP2::S4 / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][NQ * 256];
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= count) return;
-  const int prime = blockIdx.y;
-  const ModDev& md = prime ? key.q2 : key.p2;
-  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
-  uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
-  const uint32_t* mine = img + (threadIdx.x & 63) * 4;
   MP2 M;
-  M.init(prime ? Nq2 : Np2, md.n0inv);
+  M.init(Np, md.n0inv);
   uint32_t b[MP2::L];
   M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
-  M.mul(b, ARow{prime ? key.nR2_q2 : key.nR2_p2});  // n m R mod P^2
-  M.add_row(b, md.R1);                              // (1 + n m) R
+  M.mul(b, ARow{nR2});     // n m R mod P^2
+  M.add_row(b, md.R1);     // (1 + n m) R
   const uint32_t* ae = a_words + (size_t)e * aw;
   const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
@@ -317,13 +309,30 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
   M.reduce_once(b);
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
-#endif
 
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
-                                                    uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
-  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+__global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32_t* __restrict__ Np2,
+                                                        const uint32_t* __restrict__ Nq2,
+                                                        const uint32_t* __restrict__ m_words,
+                                                        const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                        uint32_t* __restrict__ ws) {
+  static_assert(MP2::TPI == 1, "LDS row staging is per lane");
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
+  const int prime = blockIdx.y;
+  uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
+  djn_prime_lds<MP2>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
+                     prime ? key.nR2_q2 : key.nR2_p2, m_words, a_words, aw, count, e, prime, img,
+                     img + (threadIdx.x & 63) * 4, ws);
+}
+
+#endif
+
+// c = c_q + q^2 ((c_p + 4p^2 - c_q) (q^2)^-1 mod p^2) for element e (utils.py:38-43)
+template <class MP2>
+XHE_DEV void crt_enc_elem(const KeyDev& key, const uint32_t* __restrict__ Np2, int64_t count, int64_t e,
+                          uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
   uint32_t* rp = ws + e;
   uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + e;
   const int st = (int)count;
@@ -335,6 +344,14 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* 
   M.mul(b, ARow{key.q2invR_p2});
   M.reduce_once(b);
   M.wide_mul_add_store(b, ARow{key.q2_lim}, rq, st, out + (size_t)e * key.n2w, key.n2w);
+}
+
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
+                                                    uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (e >= count) return;
+  crt_enc_elem<MP2>(key, Np2, count, e, ws, out);
 }
 
 // Raw encryption without obfuscation (paillier.py:283): c = 1 + n m  (m < n,
