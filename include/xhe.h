@@ -134,6 +134,20 @@ int xhe_decrypt_decode_host(const xhe_key* key, const uint32_t* ct, const int32_
 int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct);
 int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint32_t* m);
 
+/* Wire codec (host only, no device needed): the byte format of
+ * Paillier.serialize / Paillier.ciphertext_from (paillier.py:244-271,
+ * compression=False; zstd framing stays in the caller) — a pickle of an
+ * np.ndarray(dtype=object) of RawCiphertext(value, exp) — to and from flat
+ * buffers (ct: count x n2w little-endian words). encode: XHE_EOVERFLOW with
+ * *out_len = bytes needed when cap is too small (out may be NULL). decode:
+ * accepts CPython's pickles of that object graph at protocols 2-5, including
+ * the reference's gmpy2 mpz values; XHE_EOVERFLOW with *count set when
+ * cap_count is too small; XHE_EINVAL on anything else. */
+int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                    uint8_t* out, int64_t cap, int64_t* out_len);
+int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
+                    int64_t* count, int64_t* shape, int* ndim);
+
 /* Kernel timing: when enabled, the library brackets each launch of its
  * dominant kernels (k_djn_pow, k_dec_pow) with hipEvents on the launch stream.
  * xhe_profile(1) enables and clears, xhe_profile(0) disables and clears;

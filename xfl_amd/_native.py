@@ -58,6 +58,10 @@ SIGNATURES = {
     "xhe_encrypt_words_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p,
                                               ctypes.c_uint64, _vp]),
     "xhe_decrypt_decode_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
+    "xhe_wire_encode": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, _vp,
+                                       ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
+                                       ctypes.POINTER(ctypes.c_int64), _vp, ctypes.POINTER(ctypes.c_int)]),
     "xhe_profile": (ctypes.c_int, [ctypes.c_int]),
     "xhe_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64)]),
@@ -118,13 +122,10 @@ def int_to_words(x, nw):
 
 
 def ints_to_words(xs, nw):
-    out = np.empty((len(xs), nw), dtype=np.uint32)
     nb = 4 * nw
-    buf = bytearray(nb * len(xs))
-    for i, x in enumerate(xs):
-        buf[i * nb:(i + 1) * nb] = int(x).to_bytes(nb, "little")
-    out[:] = np.frombuffer(bytes(buf), dtype="<u4").reshape(len(xs), nw)
-    return out
+    tb = int.to_bytes
+    buf = bytearray().join([tb(int(x), nb, "little") for x in xs])
+    return np.frombuffer(buf, dtype="<u4").reshape(len(xs), nw)
 
 
 def words_to_ints(w):
@@ -132,8 +133,9 @@ def words_to_ints(w):
     if w.ndim == 1:
         return int.from_bytes(w.tobytes(), "little")
     nb = w.shape[1] * 4
-    raw = w.tobytes()
-    return [int.from_bytes(raw[i * nb:(i + 1) * nb], "little") for i in range(w.shape[0])]
+    mv = memoryview(w).cast("B")  # no copy
+    fb = int.from_bytes
+    return [fb(mv[i * nb:(i + 1) * nb], "little") for i in range(w.shape[0])]
 
 
 def ptr(a):

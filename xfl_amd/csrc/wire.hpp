@@ -1,0 +1,489 @@
+// Wire codec for ciphertext vectors (host code): the byte format of
+// Paillier.serialize / Paillier.ciphertext_from (paillier.py:244-271) —
+// pickle of an np.ndarray(dtype=object) of RawCiphertext(value, exp) — to and
+// from flat little-endian word buffers, without creating a Python object per
+// element.
+//
+// Encoder: protocol-4 opcodes, unframed, numpy's ndarray reduce
+// (numpy.core.multiarray._reconstruct, loadable by numpy 1.x and 2.x),
+// RawCiphertext as NEWOBJ + BUILD({'value': int, 'exp': int}) with the class
+// and the two keys memoised once; values as LONG1/LONG4.
+// Decoder: a small pickle machine for the opcodes CPython emits for that
+// object graph at protocols 2-5 (framing, memo forms, GLOBAL/STACK_GLOBAL),
+// including the reference's gmpy2 values (REDUCE of gmpy2.from_binary on
+// gmpy2's binary format: type 0x01, sign byte, little-endian magnitude).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace xhe {
+namespace wire {
+
+struct Writer {
+  uint8_t* out;
+  int64_t cap, n = 0;
+  void put(uint8_t b) {
+    if (n < cap) out[n] = b;
+    ++n;
+  }
+  void put(const void* p, int64_t len) {
+    if (n + len <= cap) memcpy(out + n, p, (size_t)len);
+    n += len;
+  }
+  void u32(uint32_t v) {
+    for (int i = 0; i < 4; ++i) put((uint8_t)(v >> (8 * i)));
+  }
+  void str(const char* s) {  // SHORT_BINUNICODE
+    size_t len = strlen(s);
+    put(0x8c);
+    put((uint8_t)len);
+    put(s, (int64_t)len);
+  }
+  void binint(int32_t v) {
+    if (v >= 0 && v < 256) {
+      put('K');
+      put((uint8_t)v);
+    } else {
+      put('J');
+      u32((uint32_t)v);
+    }
+  }
+  void binint64(int64_t v) {  // shape entries
+    if (v >= 0 && v < 256) {
+      put('K');
+      put((uint8_t)v);
+    } else if (v >= INT32_MIN && v <= INT32_MAX) {
+      put('J');
+      u32((uint32_t)v);
+    } else {
+      uint8_t b[9];
+      int len = 0;
+      for (; len < 8; ++len) b[len] = (uint8_t)((uint64_t)v >> (8 * len));
+      put(0x8a);
+      put((uint8_t)len);
+      put(b, len);
+    }
+  }
+};
+
+// non-negative little-endian words -> LONG1/LONG4 (minimal two's complement)
+inline void put_long(Writer& w, const uint32_t* words, int nw) {
+  int top = nw - 1;
+  while (top >= 0 && words[top] == 0) --top;
+  int64_t bits = 0;
+  if (top >= 0) bits = 32 * top + (32 - __builtin_clz(words[top]));
+  int64_t nbytes = bits == 0 ? 0 : (bits + 8) / 8;  // one sign bit of room
+  if (nbytes < 256) {
+    w.put(0x8a);
+    w.put((uint8_t)nbytes);
+  } else {
+    w.put(0x8b);
+    w.u32((uint32_t)nbytes);
+  }
+  // little-endian words are the little-endian bytes; at most one zero byte
+  // of sign room lies beyond the top word
+  int64_t have = std::min<int64_t>(nbytes, 4 * (int64_t)nw);
+  w.put(words, have);
+  for (int64_t i = have; i < nbytes; ++i) w.put((uint8_t)0);
+}
+
+// returns the byte count (writes only when it fits in cap)
+inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                      uint8_t* out, int64_t cap) {
+  Writer w{out, cap};
+  w.put(0x80);
+  w.put(4);
+  w.str("numpy.core.multiarray");
+  w.str("_reconstruct");
+  w.put(0x93);
+  w.str("numpy");
+  w.put(0x94);  // memo 0: 'numpy'
+  w.str("ndarray");
+  w.put(0x93);
+  w.put('K');
+  w.put(0);
+  w.put(0x85);
+  w.put('C');
+  w.put(1);
+  w.put('b');
+  w.put(0x87);
+  w.put('R');
+  w.put('(');  // state tuple
+  w.put('K');
+  w.put(1);
+  w.put('(');
+  for (int d = 0; d < ndim; ++d) w.binint64(shape[d]);
+  w.put('t');
+  w.put('h');
+  w.put(0);  // 'numpy'
+  w.str("dtype");
+  w.put(0x93);
+  w.str("O8");
+  w.put(0x89);
+  w.put(0x88);
+  w.put(0x87);
+  w.put('R');
+  w.put('(');
+  w.put('K');
+  w.put(3);
+  w.str("|");
+  w.put('N');
+  w.put('N');
+  w.put('N');
+  w.binint(-1);
+  w.binint(-1);
+  w.put('K');
+  w.put(63);
+  w.put('t');
+  w.put('b');     // dtype state
+  w.put(0x89);    // is_fortran = False
+  w.put(']');
+  for (int64_t i = 0; i < count; ++i) {
+    if (i % 1000 == 0) w.put('(');
+    if (i == 0) {
+      w.str("common.crypto.paillier.paillier");
+      w.str("RawCiphertext");
+      w.put(0x93);
+      w.put(0x94);  // memo 1: the class
+    } else {
+      w.put('h');
+      w.put(1);
+    }
+    w.put(')');
+    w.put(0x81);  // NEWOBJ
+    w.put('}');
+    w.put('(');
+    if (i == 0) {
+      w.str("value");
+      w.put(0x94);  // memo 2
+    } else {
+      w.put('h');
+      w.put(2);
+    }
+    put_long(w, ct + (size_t)i * n2w, n2w);
+    if (i == 0) {
+      w.str("exp");
+      w.put(0x94);  // memo 3
+    } else {
+      w.put('h');
+      w.put(3);
+    }
+    w.binint(exps[i]);
+    w.put('u');
+    w.put('b');
+    if (i % 1000 == 999 || i == count - 1) w.put('e');
+  }
+  w.put('t');  // state tuple
+  w.put('b');  // ndarray.__setstate__
+  w.put('.');
+  return w.n;
+}
+
+// ------------------------------------------------------------------ decoder
+struct Val {
+  enum Kind : uint8_t { NONE, BOOL, INT, BYTES, STR, TUPLE, LIST, DICT, GLOBAL, OBJ, MARK } k = NONE;
+  bool neg = false;                 // INT sign
+  int64_t off = -1, n = 0;          // payload (BYTES/STR bytes, non-negative INT magnitude) as a view of the input
+  std::string s;                    // owned payload: negative INT magnitude, GLOBAL "module name"
+  std::vector<int32_t> items;       // TUPLE/LIST elements, DICT key/value pairs
+  int32_t cls = -1, args = -1, state = -1;  // OBJ: callable/class, its args, BUILD state
+};
+
+struct Machine {
+  const uint8_t* p;
+  int64_t len, pos = 0;
+  std::vector<Val> arena;
+  std::vector<int32_t> stack, memo;
+  std::vector<size_t> marks;
+
+  std::vector<int32_t> scratch;  // pop_mark result (reused: one element's SETITEMS at a time)
+
+  explicit Machine(const uint8_t* d, int64_t l) : p(d), len(l) {
+    arena.reserve((size_t)std::min<int64_t>(l / 64 + 64, (int64_t)1 << 26));
+  }
+  [[noreturn]] void bad(const char* why) { throw std::runtime_error(std::string("wire decode: ") + why); }
+  const uint8_t* take(int64_t k) {
+    if (k < 0 || pos + k > len) bad("truncated");
+    const uint8_t* r = p + pos;
+    pos += k;
+    return r;
+  }
+  uint64_t uint_le(int k) {
+    const uint8_t* b = take(k);
+    uint64_t v = 0;
+    for (int i = 0; i < k; ++i) v |= (uint64_t)b[i] << (8 * i);
+    return v;
+  }
+  int32_t make(Val v) {
+    arena.push_back(std::move(v));
+    return (int32_t)arena.size() - 1;
+  }
+  int32_t pop() {
+    if (stack.empty() || (!marks.empty() && stack.size() <= marks.back())) bad("stack underflow");
+    int32_t v = stack.back();
+    stack.pop_back();
+    return v;
+  }
+  const std::vector<int32_t>& pop_mark() {
+    if (marks.empty()) bad("no mark");
+    size_t m = marks.back();
+    marks.pop_back();
+    scratch.assign(stack.begin() + m, stack.end());
+    stack.resize(m);
+    return scratch;
+  }
+  // two's complement LE; `in_input`: b points into the pickle (kept as a view)
+  int32_t make_int(const uint8_t* b, int64_t n, bool in_input) {
+    Val v;
+    v.k = Val::INT;
+    if (n > 0 && (b[n - 1] & 0x80)) {  // negative: magnitude = -x
+      v.neg = true;
+      std::string m((const char*)b, (size_t)n);
+      int carry = 1;
+      for (auto& c : m) {
+        int x = (uint8_t)~(uint8_t)c + carry;
+        c = (char)(x & 0xff);
+        carry = x >> 8;
+      }
+      v.s = m;
+    } else if (in_input) {
+      v.off = b - p;
+      v.n = n;
+    } else {
+      v.s.assign((const char*)b, (size_t)n);
+    }
+    return make(std::move(v));
+  }
+  int32_t make_small(int64_t x) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; ++i) b[i] = (uint8_t)((uint64_t)x >> (8 * i));
+    return make_int(b, 8, false);
+  }
+  // payload bytes of a BYTES/STR/INT value
+  std::string bytes_of(int32_t i) const {
+    const Val& v = arena[i];
+    return v.off >= 0 ? std::string((const char*)p + v.off, (size_t)v.n) : v.s;
+  }
+  bool str_eq(int32_t i, const char* lit) const {
+    const Val& v = arena[i];
+    size_t l = strlen(lit);
+    if (v.off >= 0) return (size_t)v.n == l && memcmp(p + v.off, lit, l) == 0;
+    return v.s == lit;
+  }
+  void put_memo(uint64_t i, int32_t v) {
+    if (i > (1u << 26)) bad("memo index");
+    if (memo.size() <= i) memo.resize(i + 1, -1);
+    memo[i] = v;
+  }
+  int32_t get_memo(uint64_t i) {
+    if (i >= memo.size() || memo[i] < 0) bad("memo miss");
+    return memo[i];
+  }
+  std::string line() {
+    int64_t s = pos;
+    while (pos < len && p[pos] != '\n') ++pos;
+    if (pos >= len) bad("truncated line");
+    std::string r((const char*)p + s, (size_t)(pos - s));
+    ++pos;
+    return r;
+  }
+
+  int32_t run() {
+    while (true) {
+      uint8_t op = *take(1);
+      switch (op) {
+        case 0x80: take(1); break;                  // PROTO
+        case 0x95: take(8); break;                  // FRAME (framing is transparent)
+        case '.': return pop();                     // STOP
+        case '(': marks.push_back(stack.size()); break;
+        case ')': { Val v; v.k = Val::TUPLE; stack.push_back(make(v)); break; }
+        case 't': { Val v; v.k = Val::TUPLE; v.items = pop_mark(); stack.push_back(make(std::move(v))); break; }
+        case 0x85: case 0x86: case 0x87: {          // TUPLE1..3
+          int k = op - 0x84;
+          Val v;
+          v.k = Val::TUPLE;
+          v.items.resize(k);
+          for (int i = k - 1; i >= 0; --i) v.items[i] = pop();
+          stack.push_back(make(std::move(v)));
+          break;
+        }
+        case ']': { Val v; v.k = Val::LIST; stack.push_back(make(v)); break; }
+        case '}': { Val v; v.k = Val::DICT; stack.push_back(make(v)); break; }
+        case 'a': {
+          int32_t x = pop();
+          arena[stack.back()].items.push_back(x);
+          break;
+        }
+        case 'e': {
+          const auto& xs = pop_mark();
+          if (stack.empty()) bad("appends target");
+          auto& l = arena[stack.back()].items;
+          l.insert(l.end(), xs.begin(), xs.end());
+          break;
+        }
+        case 's': {
+          int32_t v = pop(), k = pop();
+          auto& d = arena[stack.back()].items;
+          d.push_back(k);
+          d.push_back(v);
+          break;
+        }
+        case 'u': {
+          const auto& xs = pop_mark();
+          if (stack.empty() || xs.size() % 2) bad("setitems");
+          auto& d = arena[stack.back()].items;
+          d.insert(d.end(), xs.begin(), xs.end());
+          break;
+        }
+        case 'N': { Val v; stack.push_back(make(v)); break; }
+        case 0x88: case 0x89: { Val v; v.k = Val::BOOL; v.neg = op == 0x88; stack.push_back(make(v)); break; }
+        case 'J': stack.push_back(make_small((int32_t)uint_le(4))); break;
+        case 'K': stack.push_back(make_small((int64_t)uint_le(1))); break;
+        case 'M': stack.push_back(make_small((int64_t)uint_le(2))); break;
+        case 0x8a: { int64_t n = (int64_t)uint_le(1); stack.push_back(make_int(take(n), n, true)); break; }
+        case 0x8b: { int64_t n = (int64_t)(int32_t)uint_le(4); stack.push_back(make_int(take(n), n, true)); break; }
+        case 0x8c: case 'X': case 0x8d: case 'C': case 'B': case 0x8e: {
+          int lb = (op == 0x8c || op == 'C') ? 1 : (op == 'X' || op == 'B') ? 4 : 8;
+          int64_t n = (int64_t)uint_le(lb);
+          Val v;
+          v.k = (op == 0x8c || op == 'X' || op == 0x8d) ? Val::STR : Val::BYTES;
+          v.off = take(n) - p;
+          v.n = n;
+          stack.push_back(make(std::move(v)));
+          break;
+        }
+        case 'G': { take(8); Val v; stack.push_back(make(v)); break; }  // BINFLOAT: not part of the format
+        case 'c': {  // GLOBAL
+          Val v;
+          v.k = Val::GLOBAL;
+          v.s = line();
+          v.s += " " + line();
+          stack.push_back(make(std::move(v)));
+          break;
+        }
+        case 0x93: {  // STACK_GLOBAL
+          int32_t name = pop(), mod = pop();
+          if (arena[name].k != Val::STR || arena[mod].k != Val::STR) bad("stack_global");
+          Val v;
+          v.k = Val::GLOBAL;
+          v.s = bytes_of(mod) + " " + bytes_of(name);
+          stack.push_back(make(std::move(v)));
+          break;
+        }
+        case 'R': case 0x81: {  // REDUCE / NEWOBJ
+          int32_t args = pop(), cls = pop();
+          Val v;
+          v.k = Val::OBJ;
+          v.cls = cls;
+          v.args = args;
+          stack.push_back(make(std::move(v)));
+          break;
+        }
+        case 'b': {
+          int32_t st = pop();
+          if (stack.empty()) bad("build target");
+          arena[stack.back()].state = st;
+          break;
+        }
+        case 0x94: if (stack.empty()) bad("memoize"); put_memo(memo.size(), stack.back()); break;
+        case 'q': if (stack.empty()) bad("binput"); put_memo(uint_le(1), stack.back()); break;
+        case 'r': if (stack.empty()) bad("long_binput"); put_memo(uint_le(4), stack.back()); break;
+        case 'h': stack.push_back(get_memo(uint_le(1))); break;
+        case 'j': stack.push_back(get_memo(uint_le(4))); break;
+        default: bad("unsupported opcode");
+      }
+    }
+  }
+};
+
+inline bool is_global(const Machine& m, int32_t v, const char* mod_name) {
+  return v >= 0 && m.arena[v].k == Val::GLOBAL && m.arena[v].s == mod_name;
+}
+
+// little-endian magnitude bytes -> n2w words (false if it does not fit)
+inline bool mag_to_words(const std::string& mag, uint32_t* w, int n2w) {
+  for (int i = 0; i < n2w; ++i) w[i] = 0;
+  for (size_t i = 0; i < mag.size(); ++i) {
+    uint8_t b = (uint8_t)mag[i];
+    if (!b) continue;
+    if (i / 4 >= (size_t)n2w) return false;
+    w[i / 4] |= (uint32_t)b << (8 * (i % 4));
+  }
+  return true;
+}
+
+inline int32_t dict_get(const Machine& m, int32_t d, const char* key) {
+  const auto& it = m.arena[d].items;
+  for (size_t i = 0; i + 1 < it.size(); i += 2)
+    if (m.arena[it[i]].k == Val::STR && m.str_eq(it[i], key)) return it[i + 1];
+  return -1;
+}
+
+inline int64_t int_value(const Machine& m, int32_t v) {
+  const Val& x = m.arena[v];
+  if (x.k != Val::INT) throw std::runtime_error("wire decode: expected an int");
+  std::string b = m.bytes_of(v);
+  size_t n = b.size();
+  while (n > 0 && b[n - 1] == 0) --n;
+  if (n > 8) throw std::runtime_error("wire decode: int out of range");
+  uint64_t u = 0;
+  for (size_t i = 0; i < n; ++i) u |= (uint64_t)(uint8_t)b[i] << (8 * i);
+  if (u > (uint64_t)INT64_MAX) throw std::runtime_error("wire decode: int out of range");
+  return x.neg ? -(int64_t)u : (int64_t)u;
+}
+
+// Decodes into ct [count][n2w], exps [count]; shape/ndim of the array.
+// Returns the element count; throws on any deviation from the format.
+inline int64_t decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
+                      int64_t* shape, int* ndim) {
+  Machine m(data, len);
+  int32_t top = m.run();
+  const Val& arr = m.arena[top];
+  if (arr.k != Val::OBJ || arr.state < 0) throw std::runtime_error("wire decode: not an ndarray pickle");
+  const Val& st = m.arena[arr.state];
+  if (st.k != Val::TUPLE || st.items.size() != 5) throw std::runtime_error("wire decode: ndarray state");
+  const Val& shp = m.arena[st.items[1]];
+  const Val& lst = m.arena[st.items[4]];
+  if (shp.k != Val::TUPLE || lst.k != Val::LIST || shp.items.size() > 8)
+    throw std::runtime_error("wire decode: ndarray state");
+  *ndim = (int)shp.items.size();
+  for (int d = 0; d < *ndim; ++d) shape[d] = int_value(m, shp.items[d]);
+  const int64_t count = (int64_t)lst.items.size();
+  if (count > cap_count) return count;  // caller retries with room
+  for (int64_t i = 0; i < count; ++i) {
+    const Val& o = m.arena[lst.items[i]];
+    if (o.k != Val::OBJ || o.state < 0 || !is_global(m, o.cls, "common.crypto.paillier.paillier RawCiphertext"))
+      throw std::runtime_error("wire decode: element is not a RawCiphertext");
+    int32_t val = dict_get(m, o.state, "value"), ex = dict_get(m, o.state, "exp");
+    if (val < 0 || ex < 0) throw std::runtime_error("wire decode: RawCiphertext state");
+    const Val* v = &m.arena[val];
+    std::string mag;
+    if (v->k == Val::INT) {
+      if (v->neg) throw std::runtime_error("wire decode: negative ciphertext");
+      mag = m.bytes_of(val);
+    } else if (v->k == Val::OBJ && is_global(m, v->cls, "gmpy2 from_binary")) {
+      const Val& a = m.arena[v->args];
+      if (a.k != Val::TUPLE || a.items.size() != 1 || m.arena[a.items[0]].k != Val::BYTES)
+        throw std::runtime_error("wire decode: gmpy2 value");
+      const std::string b = m.bytes_of(a.items[0]);
+      if (b.size() < 2 || (uint8_t)b[0] != 0x01) throw std::runtime_error("wire decode: gmpy2 binary type");
+      if ((uint8_t)b[1] == 0x02) throw std::runtime_error("wire decode: negative ciphertext");
+      mag = b.substr(2);
+    } else {
+      throw std::runtime_error("wire decode: value type");
+    }
+    if (!mag_to_words(mag, ct + (size_t)i * n2w, n2w)) throw std::runtime_error("wire decode: value too large");
+    int64_t e = int_value(m, ex);
+    if (e < INT32_MIN || e > INT32_MAX) throw std::runtime_error("wire decode: exponent range");
+    exps[i] = (int32_t)e;
+  }
+  return count;
+}
+
+}  // namespace wire
+}  // namespace xhe

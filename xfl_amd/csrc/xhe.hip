@@ -13,6 +13,7 @@
 
 #include "../../include/xhe.h"
 #include "hostbn.hpp"
+#include "wire.hpp"
 #include "xhe_kernels.hpp"
 
 using namespace xhe;
@@ -1280,6 +1281,34 @@ int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases,
     if (rc != XHE_OK) return rc;
     HIPCHK(hipMemcpyAsync(out, dout.p, (size_t)ncols * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
     HIPCHK(hipStreamSynchronize(st.s));
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                    uint8_t* out, int64_t cap, int64_t* out_len) {
+  return guarded([&]() -> int {
+    if (!out_len || count < 0 || n2w <= 0 || ndim < 0 || ndim > 8 || (count > 0 && (!ct || !exps)) ||
+        (ndim > 0 && !shape))
+      return fail(XHE_EINVAL, "xhe_wire_encode: bad argument");
+    int64_t prod = 1;
+    for (int d = 0; d < ndim; ++d) prod *= shape[d];
+    if (prod != count) return fail(XHE_EINVAL, "xhe_wire_encode: shape does not match count");
+    int64_t need = wire::encode(ct, exps, count, n2w, shape, ndim, out, out ? cap : 0);
+    *out_len = need;
+    if (!out || need > cap) return fail(XHE_EOVERFLOW, "xhe_wire_encode: output buffer too small");
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
+                    int64_t* count, int64_t* shape, int* ndim) {
+  return guarded([&]() -> int {
+    if (!data || len <= 0 || n2w <= 0 || !count || !shape || !ndim || (cap_count > 0 && (!ct || !exps)))
+      return fail(XHE_EINVAL, "xhe_wire_decode: bad argument");
+    int64_t n = wire::decode(data, len, n2w, ct, exps, cap_count, shape, ndim);
+    *count = n;
+    if (n > cap_count) return fail(XHE_EOVERFLOW, "xhe_wire_decode: output buffers too small");
     return XHE_OK;
   });
 }

@@ -49,6 +49,8 @@ class PaillierCiphertext(object):
     materializes (materialize() does a whole array in one call).
     """
 
+    __slots__ = ("_PaillierCiphertext__context", "_PaillierCiphertext__c", "_PaillierCiphertext__exp", "_parts")
+
     def __init__(self, context: PaillierContext, raw_ciphertext: MPZ, exponent: int) -> None:
         self.__context = context
         self.__c = None if raw_ciphertext is None else int(raw_ciphertext)
@@ -222,7 +224,15 @@ class Paillier(object):
             return data.serialize(compression)
 
         if isinstance(data, np.ndarray) and data.dtype == object:
-            materialize(list(data.reshape(-1)))
+            flat = list(data.reshape(-1))
+            materialize(flat)
+            if flat and all(isinstance(x, PaillierCiphertext) for x in flat):
+                from . import wire
+                raws = [x.raw_ciphertext for x in flat]
+                ctx = flat[0].context
+                bits = ctx.n_square.bit_length() if ctx is not None else max(r.bit_length() for r in raws)
+                out = wire.encode(raws, [x.exponent for x in flat], data.shape, max(1, (bits + 31) // 32))
+                return compress(out) if compression else out
 
         def f(x):
             return RawCiphertext(x.raw_ciphertext, x.exponent)
@@ -234,14 +244,24 @@ class Paillier(object):
     def ciphertext_from(context: PaillierContext, data: bytes, compression: bool = True):
         """paillier.py:260-271"""
         from ..compat import decompress, loads
+        from .array import PaillierArray
         if compression:
             data = decompress(data)
+        try:  # native decode of the ciphertext-array format
+            from . import wire
+            n2w = (context.n_square.bit_length() + 31) // 32 if context is not None else None
+            raws, exps, shape = wire.decode(data, n2w)
+            out = np.empty(len(raws), dtype=object)
+            for i, (r, e) in enumerate(zip(raws, exps.tolist())):
+                out[i] = PaillierCiphertext(context, r, e)
+            return out.reshape(shape).view(PaillierArray)
+        except ValueError:
+            pass
         unpickled = loads(data)
 
         def f(x):
             return PaillierCiphertext(context, int(x.value), x.exp)
 
-        from .array import PaillierArray
         return np.vectorize(f, otypes=[PaillierCiphertext])(unpickled).view(PaillierArray)
 
     @classmethod
