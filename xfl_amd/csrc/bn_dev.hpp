@@ -34,6 +34,9 @@ namespace xhe {
 #ifndef XHE_LDS_ROWS
 #define XHE_LDS_ROWS 1  // k_djn_pow_lds: table rows staged in LDS by LDS-DMA bursts
 #endif
+#ifndef XHE_SQ_LDS
+#define XHE_SQ_LDS 1  // variable-base exponentiations: squaring operand through LDS (SqLds)
+#endif
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif

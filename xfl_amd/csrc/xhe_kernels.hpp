@@ -381,9 +381,45 @@ __global__ void __launch_bounds__(256, 2) k_raw_enc(KeyDev key, const uint32_t* 
 // k_dec_pow: X_P = (c^(P-1) mod P^2) - 1 for one prime (grid.y), written to
 // xrows [prime][S4][count]. Per-group 4-bit window tables live in wsg
 // (17 interleaved rows per group, grid-stride loop over elements).
+// The squaring operand of an exponentiation, parked in LDS instead of a
+// global workspace row (a squaring reads back the 74-152 limbs it just
+// wrote: through LDS that round trip never leaves the CU). Per wave: 64 / TPI
+// residues of S4 words. TPI == 1: quad-major image [quad][lane][4 words]
+// (ds_write_b128 / ds_read_b128, conflict-free); TPI > 1: one contiguous row
+// per lane group, read by the whole group (broadcast).
+template <class M_>
+struct SqLds {
+  static constexpr int WORDS_PER_WAVE = 64 / M_::TPI * M_::S4;
+  uint32_t* slot;
+  XHE_DEV explicit SqLds(uint32_t* wave_img) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (M_::TPI == 1) slot = wave_img + lane * 4;
+    else slot = wave_img + (lane / M_::TPI) * M_::S4;
+  }
+  XHE_DEV void put(const uint32_t (&b)[M_::L]) const {
+    if constexpr (M_::TPI == 1) {
+#pragma unroll
+      for (int q = 0; q < M_::S4 / 4; ++q) {
+        uint4 v = make_uint4(4 * q < M_::S ? b[4 * q] : 0u, 4 * q + 1 < M_::S ? b[4 * q + 1] : 0u,
+                             4 * q + 2 < M_::S ? b[4 * q + 2] : 0u, 4 * q + 3 < M_::S ? b[4 * q + 3] : 0u);
+        *reinterpret_cast<uint4*>(slot + q * 256) = v;
+      }
+    } else {
+      const int g = M_::G::g();
+#pragma unroll
+      for (int j = 0; j < M_::L; ++j) slot[g * M_::L + j] = b[j];
+    }
+    wave_sync_mem_();
+  }
+  XHE_DEV uint4 load4(int i) const {
+    if constexpr (M_::TPI == 1) return *reinterpret_cast<const uint4*>(slot + (i >> 2) * 256);
+    else return *reinterpret_cast<const uint4*>(slot + i);
+  }
+};
+
 template <class MP2>
 XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* ex, int ebits,
-                             uint32_t* tab, uint32_t* sq, int st) {
+                             uint32_t* tab, uint32_t* sq, int st, uint32_t* sq_lds = nullptr) {
   const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
   M.store_strided(b, tab + rs, st);         // tab[1] = b
   wave_sync_mem_();
@@ -400,9 +436,15 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   for (int w = top - 1; w >= 0; --w) {
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
-      M.store_strided(b, sq, st);
-      wave_sync_mem_();
-      M.mul(b, AStrided{sq, st});
+      if (sq_lds) {
+        const SqLds<MP2> L(sq_lds);
+        L.put(b);
+        M.mul(b, L);
+      } else {
+        M.store_strided(b, sq, st);
+        wave_sync_mem_();
+        M.mul(b, AStrided{sq, st});
+      }
     }
     uint32_t dw = (ex[(w * 4) >> 5] >> ((w * 4) & 31)) & 15u;
     if (dw) M.mul(b, AStrided{tab + rs * dw, st});
@@ -428,6 +470,12 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
   uint32_t* tab = ws + (size_t)prime * 17 * rs + gid0;  // rows 0..15
   uint32_t* sq = tab + 16 * rs;
   const int n2w = key.n2w;
+#if XHE_SQ_LDS
+  __shared__ __attribute__((aligned(16))) uint32_t sq_img[4][SqLds<MP2>::WORDS_PER_WAVE];  // 256-thread blocks
+  uint32_t* sq_lds = sq_img[(threadIdx.x >> 6) & 3];
+#else
+  uint32_t* sq_lds = nullptr;
+#endif
   for (int64_t e = gid0; e < count; e += G_total) {
     const uint32_t* cw = c_words + (size_t)e * n2w;
     MP2 M;
@@ -450,7 +498,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
     wave_sync_mem_();
     M.redc_wide(b, AStrided{sq, st});
     M.mul(b, ARow{md.R3});
-    pow_uniform_exp(M, b, ex, ebits, tab, sq, st);
+    pow_uniform_exp(M, b, ex, ebits, tab, sq, st, sq_lds);
     M.mul(b, AOne{});
     M.reduce_once(b);  // x = c^(P-1) mod P^2, x = 1 (mod P)
     // X = x - 1 = x + (2^(W S) - 1) - 2^(W S): add all-ones, drop the top carry
@@ -540,7 +588,7 @@ XHE_DEV void store_packed(const M_& M, const uint32_t (&b)[M_::L], uint32_t* row
 // `digit(w)` (uniform inside a lane group). tab: 16 interleaved rows, sq: one.
 template <class M_, class DigitF>
 XHE_DEV void pow_window4(const M_& M, uint32_t (&b)[M_::L], const uint32_t* R1, int nwin, DigitF digit,
-                         uint32_t* tab, uint32_t* sq, int st) {
+                         uint32_t* tab, uint32_t* sq, int st, uint32_t* sq_lds = nullptr) {
   const size_t rs = (size_t)M_::S4 * st;
   M.store_strided(b, tab + rs, st);  // tab[1] = b
   {
@@ -560,9 +608,15 @@ XHE_DEV void pow_window4(const M_& M, uint32_t (&b)[M_::L], const uint32_t* R1, 
   for (int w = nwin - 2; w >= 0; --w) {
 #pragma unroll 1
     for (int s = 0; s < 4; ++s) {
-      M.store_strided(b, sq, st);
-      wave_sync_mem_();
-      M.mul(b, AStrided{sq, st});
+      if (sq_lds) {
+        const SqLds<M_> L(sq_lds);
+        L.put(b);
+        M.mul(b, L);
+      } else {
+        M.store_strided(b, sq, st);
+        wave_sync_mem_();
+        M.mul(b, AStrided{sq, st});
+      }
     }
     M.mul(b, AStrided{tab + rs * digit(w), st});
   }
@@ -636,6 +690,12 @@ __global__ void __launch_bounds__(256, 2) k_powmod_n2(KeyDev key, const uint32_t
   uint32_t* tab = ws + gid0;
   uint32_t* sq = tab + 16 * rs;
   const int nwin = kbits <= 0 ? 1 : (kbits + 3) / 4;
+#if XHE_SQ_LDS
+  __shared__ __attribute__((aligned(16))) uint32_t sq_img[4][SqLds<MN2>::WORDS_PER_WAVE];  // 256-thread blocks
+  uint32_t* sq_lds = sq_img[(threadIdx.x >> 6) & 3];
+#else
+  uint32_t* sq_lds = nullptr;
+#endif
   for (int64_t e = gid0; e < count; e += G_total) {
     MN2 M;
     M.init(Nn2, key.n2.n0inv);
@@ -643,7 +703,7 @@ __global__ void __launch_bounds__(256, 2) k_powmod_n2(KeyDev key, const uint32_t
     M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
     M.mul(b, ARow{key.n2.R2});
     const uint32_t* ke = k + (size_t)e * kw;
-    pow_window4(M, b, key.n2.R1, nwin, [&](int w) { return nibble(ke, kw, w); }, tab, sq, st);
+    pow_window4(M, b, key.n2.R1, nwin, [&](int w) { return nibble(ke, kw, w); }, tab, sq, st, sq_lds);
     M.mul(b, AOne{});
     M.reduce_once(b);
     store_packed(M, b, sq, st, out + (size_t)e * key.n2w, key.n2w);
@@ -684,7 +744,8 @@ __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* 
 template <class M_>
 XHE_DEV void nodjn_core(const M_& M, uint32_t (&b)[M_::L], const ModDev& md, const uint32_t* nR2,
                         const uint32_t* mw, int nw, const uint32_t* rw, int rwn, const uint32_t* ex, int exw,
-                        int ebits, uint32_t* tab, uint32_t* sq, uint32_t* park, int st) {
+                        int ebits, uint32_t* tab, uint32_t* sq, uint32_t* park, int st,
+                        uint32_t* sq_lds = nullptr) {
   // c0 R = (1 + n m) R parked first
   M.load_words(b, mw, nw);
   M.mul(b, ARow{nR2});
@@ -694,7 +755,7 @@ XHE_DEV void nodjn_core(const M_& M, uint32_t (&b)[M_::L], const ModDev& md, con
   M.load_words(b, rw, rwn);
   M.mul(b, ARow{md.R2});
   const int nwin = (ebits + 3) / 4;
-  pow_window4(M, b, md.R1, nwin, [&](int w) { return nibble(ex, exw, w); }, tab, sq, st);
+  pow_window4(M, b, md.R1, nwin, [&](int w) { return nibble(ex, exw, w); }, tab, sq, st, sq_lds);
   wave_sync_mem_();
   M.mul(b, AStrided{park, st});
   M.mul(b, AOne{});
@@ -711,12 +772,18 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_pub(KeyDev key, const uint32_t
   const int st = (int)G_total;
   const size_t rs = (size_t)MN2::S4 * st;
   uint32_t* tab = ws + gid0;
+#if XHE_SQ_LDS
+  __shared__ __attribute__((aligned(16))) uint32_t sq_img[4][SqLds<MN2>::WORDS_PER_WAVE];  // 256-thread blocks
+  uint32_t* sq_lds = sq_img[(threadIdx.x >> 6) & 3];
+#else
+  uint32_t* sq_lds = nullptr;
+#endif
   for (int64_t e = gid0; e < count; e += G_total) {
     MN2 M;
     M.init(Nn2, key.n2.n0inv);
     uint32_t b[MN2::L];
     nodjn_core(M, b, key.n2, key.nR2_n2, m_words + (size_t)e * key.nw, key.nw, r_words + (size_t)e * rw, rw,
-               key.n_words, key.nw, key.n_bits, tab, tab + 16 * rs, tab + 17 * rs, st);
+               key.n_words, key.nw, key.n_bits, tab, tab + 16 * rs, tab + 17 * rs, st, sq_lds);
     store_packed(M, b, tab + 16 * rs, st, out + (size_t)e * key.n2w, key.n2w);
   }
 }
@@ -734,13 +801,19 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t
   const int st = (int)G_total;
   const size_t rs = (size_t)MP2::S4 * st;
   uint32_t* tab = ws + (size_t)prime * 18 * rs + gid0;
+#if XHE_SQ_LDS
+  __shared__ __attribute__((aligned(16))) uint32_t sq_img[4][SqLds<MP2>::WORDS_PER_WAVE];  // 256-thread blocks
+  uint32_t* sq_lds = sq_img[(threadIdx.x >> 6) & 3];
+#else
+  uint32_t* sq_lds = nullptr;
+#endif
   for (int64_t e = gid0; e < count; e += G_total) {
     MP2 M;
     M.init(prime ? Nq2 : Np2, md.n0inv);
     uint32_t b[MP2::L];
     nodjn_core(M, b, md, prime ? key.nR2_q2 : key.nR2_p2, m_words + (size_t)e * key.nw, key.nw,
                r_words + (size_t)e * rw, rw, prime ? key.eq_words : key.ep_words, key.nw,
-               prime ? key.eq_bits : key.ep_bits, tab, tab + 16 * rs, tab + 17 * rs, st);
+               prime ? key.eq_bits : key.ep_bits, tab, tab + 16 * rs, tab + 17 * rs, st, sq_lds);
     M.store_strided(b, rows + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
   }
 }
