@@ -420,34 +420,56 @@ struct SqLds {
 template <class MP2>
 XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* ex, int ebits,
                              uint32_t* tab, uint32_t* sq, int st, uint32_t* sq_lds = nullptr) {
+  // 5-bit sliding window over an exponent shared by every lane (p-1 / q-1),
+  // so the square/multiply schedule is wave-uniform: odd powers
+  // tab[t] = b^(2t+1), t < 16, then ~ebits squarings and ~ebits/6 products
+  // (4-bit fixed windows: ebits/4).
   const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
-  M.store_strided(b, tab + rs, st);         // tab[1] = b
+  auto square = [&]() {
+    if (sq_lds) {
+      const SqLds<MP2> L(sq_lds);
+      L.put(b);
+      M.mul(b, L);
+    } else {
+      M.store_strided(b, sq, st);
+      wave_sync_mem_();
+      M.mul(b, AStrided{sq, st});
+    }
+  };
+  auto bit = [&](int i) { return (ex[i >> 5] >> (i & 31)) & 1u; };
+  M.store_strided(b, tab, st);  // tab[0] = b
+  square();                     // b^2, parked in the sq row
+  M.store_strided(b, sq, st);
   wave_sync_mem_();
+  M.load_strided(b, tab, st);
 #pragma unroll 1
-  for (int t = 2; t < 16; ++t) {
-    M.mul(b, AStrided{tab + rs, st});  // tab[t] = tab[t-1] * tab[1]
+  for (int t = 1; t < 16; ++t) {
+    M.mul(b, AStrided{sq, st});  // b^(2t+1) = b^(2t-1) * b^2
     M.store_strided(b, tab + rs * t, st);
   }
   wave_sync_mem_();
-  int nwin = (ebits + 3) / 4;
-  int top = nwin - 1;
-  uint32_t d = (ex[(top * 4) >> 5] >> ((top * 4) & 31)) & 15u;
-  M.load_strided(b, tab + rs * d, st);  // top window is nonzero
-  for (int w = top - 1; w >= 0; --w) {
+  bool first = true;
+  int i = ebits - 1;
 #pragma unroll 1
-    for (int s = 0; s < 4; ++s) {
-      if (sq_lds) {
-        const SqLds<MP2> L(sq_lds);
-        L.put(b);
-        M.mul(b, L);
-      } else {
-        M.store_strided(b, sq, st);
-        wave_sync_mem_();
-        M.mul(b, AStrided{sq, st});
-      }
+  while (i >= 0) {
+    if (!bit(i)) {
+      if (!first) square();
+      --i;
+      continue;
     }
-    uint32_t dw = (ex[(w * 4) >> 5] >> ((w * 4) & 31)) & 15u;
-    if (dw) M.mul(b, AStrided{tab + rs * dw, st});
+    int j = i - 4 < 0 ? 0 : i - 4;
+    while (!bit(j)) ++j;  // window [i..j] ends in a set bit
+    uint32_t val = 0;
+    for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+    if (first) {
+      M.load_strided(b, tab + rs * (val >> 1), st);
+      first = false;
+    } else {
+#pragma unroll 1
+      for (int k = i; k >= j; --k) square();
+      M.mul(b, AStrided{tab + rs * (val >> 1), st});
+    }
+    i = j - 1;
   }
 }
 
