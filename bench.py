@@ -82,6 +82,22 @@ def cpu_baseline(bits, seconds, cores):
                       f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
 
 
+def table_bytes(bits, win):
+    """Device bytes of the two fixed-base tables (xhe_key_create, include/xhe.h):
+    ceil(rand_bits/win) windows x 2^win rows x S4 words per prime, S4 the
+    radix-2^28 limb count of P^2 rounded up to 4."""
+    rand_bits = bits // 2
+    s4 = -(-(-(-(bits + 4) // 28)) // 4) * 4
+    return 2 * -(-rand_bits // win) * (1 << win) * s4 * 4
+
+
+def pick_window(bits, free_bytes, margin=16 << 30):
+    for w in (23, 22):
+        if table_bytes(bits, w) + margin <= free_bytes:
+            return w
+    return 20
+
+
 def pmc_traffic(win, n):
     """HBM bytes per k_djn_pow launch from the committed rocprofv3 PMC passes
     (tools/profile_box.sh -> tools/pmc_traffic.py), when they were taken on
@@ -210,7 +226,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
     ap.add_argument("--key-bits", type=int, default=2048)
-    ap.add_argument("--win", type=int, default=22, help="fixed-base window bits (22: 2 x 57 GB tables, 47 products per prime)")
+    ap.add_argument("--win", type=int, default=0,
+                    help="fixed-base window bits; 0 = the widest of 23 (2 x 114.8 GB tables, 45 products per prime) "
+                         "and 22 (2 x 59.9 GB, 47) whose tables leave 16 GiB of the GPU free")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
@@ -229,6 +247,8 @@ def main():
 
     bits = args.key_bits
     p, q, n, h = make_key(bits, seed=2024)
+    if args.win == 0:
+        args.win = pick_window(bits, torch.cuda.mem_get_info(local)[0])
     t_key = time.time()
     dk = nat.DeviceKey(bits, n, p, q, h, device=local, win_bits=args.win)
     torch.cuda.synchronize()

@@ -32,10 +32,11 @@ typedef struct xhe_key xhe_key;
  * (PaillierContext.init, context.py:28-71) and, for a DJN private key, the
  * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win_bits rows per window).
  * p_words/q_words NULL => public key (n only). h_pow_n_words NULL => DJN off.
- * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in [2, 22];
+ * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in [2, 24];
  * 0 = default (16, or $XHE_WIN_BITS). Tables take ceil(rand_bits/win) x
- * 2^win rows of S4 words per prime: 2048-bit key, win 16: 2 x 1.27 GB;
- * win 20: 2 x 16.1 GB (52 instead of 64 products per prime). */
+ * 2^win rows of S4 words per prime: 2048-bit key, win 16: 2 x 1.28 GB;
+ * win 20: 2 x 16.6 GB (52 instead of 64 products per prime); win 22:
+ * 2 x 59.9 GB (47); win 23: 2 x 114.8 GB (45). */
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
 void xhe_key_destroy(xhe_key* key);

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-prof}
 mkdir -p "$OUT"
 N=${N:-1000000}
-WIN=${WIN:-22}
+WIN=${WIN:-23}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
   python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-ops --n "$N" --win "$WIN" > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 for C in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES" "SQ_INSTS_SALU SQ_INSTS_SMEM"; do

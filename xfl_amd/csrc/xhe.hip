@@ -843,8 +843,8 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
       const char* ev = getenv("XHE_WIN_BITS");
       win_bits = ev ? atoi(ev) : 16;
     }
-    if (win_bits < 2 || win_bits > 22)
-      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be in [2, 22]");
+    if (win_bits < 2 || win_bits > 24)
+      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be in [2, 24]");
     std::unique_ptr<xhe_key> k(new xhe_key());
     k->device = device;
     k->K = key_bits;
