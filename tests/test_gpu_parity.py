@@ -98,3 +98,23 @@ def test_host_encrypt_chunking_is_invisible():
         mi = O.encode_element(ok, float(x[i]), 7)[0]
         ai = nat.words_to_ints(r[i].cpu().numpy().view(np.uint32))
         assert nat.words_to_ints(ct[i]) == O.encrypt_m(ok, mi, ai)
+
+
+@pytest.mark.parametrize("fx", FIXTURES)
+@pytest.mark.parametrize("count", [1, 300, 5000, 20000, 30000])
+def test_decrypt_shapes_bit_exact(fx, count):
+    """The decrypt exponentiation runs in three lane shapes chosen by batch
+    size (16 lanes per residue up to 5,120 elements, 4 up to 28,672, then 1):
+    the golden ciphertexts tiled to each regime decrypt to the golden m."""
+    from xfl_amd._native import ints_to_words, words_to_ints
+    g = load_fixture(fx)
+    dk = _dkey(g)
+    raws, ms = [], []
+    for case in ("priv_f32_p7", "priv_packed_p0", "pub_i32_none"):
+        enc, dec = g["encrypt"][case], g["decrypt"][case]
+        raws += [hx(r) for r in enc["raw"]]
+        ms += [hx(m) for m in dec["m"][len(dec["m"]) - len(enc["raw"]):]]
+    reps = -(-count // len(raws))
+    cw = ints_to_words((raws * reps)[:count], dk.n2w)
+    out = words_to_ints(dk.decrypt_words(cw))
+    assert out == (ms * reps)[:count]

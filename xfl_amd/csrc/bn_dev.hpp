@@ -1,7 +1,7 @@
 // Device multi-precision Montgomery arithmetic for gfx950 (CDNA4).
 //
 // Representation: a residue mod M is S limbs of W bits (W = 27/28) held one
-// limb per 32-bit VGPR. A group of TPI consecutive lanes (TPI in {1,2,4})
+// limb per 32-bit VGPR. A group of TPI consecutive lanes (TPI in {1,2,4,16})
 // owns one residue, lane g holding limbs [g*L, (g+1)*L), L = S/TPI.
 //
 // The Montgomery product is operand scanning with LAZY carries: the running
@@ -11,7 +11,9 @@
 // along its anti-diagonal, so 2S * 2^(2W) < 2^64 is the only constraint
 // (static_assert below). The divide-by-2^W shift is folded into the mad
 // destinations (T[j-1] = T[j] + a_i*b[j] + m*N[j]) and across lanes it is a
-// single DPP quad_perm move, so the inner loop is 2L mads + O(1) per limb of a.
+// single DPP move (quad_perm inside 2/4-lane groups, row_shl/row_shr and
+// row_newbcast inside a 16-lane DPP row), so the inner loop is 2L mads + O(1)
+// per limb of a.
 //
 // R = 2^(W*S) >= 16*M for every modulus we instantiate, so products of inputs
 // below 2M (and up to ~R/M times larger for one operand) stay below 2M and no
@@ -37,6 +39,9 @@ namespace xhe {
 #ifndef XHE_SQ_LDS
 #define XHE_SQ_LDS 1  // variable-base exponentiations: squaring operand through LDS (SqLds)
 #endif
+#ifndef XHE_M_MAD
+#define XHE_M_MAD 0  // Montgomery digit m = x0 * n0inv by v_mad_u64_u32 instead of v_mul_lo_u32
+#endif
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif
@@ -55,39 +60,49 @@ XHE_DEV uint64_t mad64s(uint32_t a, uint32_t b_uniform, uint64_t c) {
 }
 
 // ------------------------------------------------------------ lane groups
+// DPP controls: quad_perm [a,b,c,d] = a | b<<2 | c<<4 | d<<6; row_shl:1 0x101
+// (lane i <- lane i+1 of its 16-lane row), row_shr:1 0x111 (lane i <- lane
+// i-1), row_newbcast:k 0x150+k (lane k of the row to the whole row, gfx90a+).
 template <int TPI>
 struct Grp {
+  static_assert(TPI == 1 || TPI == 2 || TPI == 4 || TPI == 16, "lane groups of 1, 2, 4 or 16");
   static XHE_DEV int g() { return TPI == 1 ? 0 : (int)(threadIdx.x & (TPI - 1)); }
 
+  // (mov_dpp with bound_ctrl: a source lane outside the 16-lane row reads 0,
+  // and no "old" value has to be materialised first)
+  template <int CTRL>
+  static XHE_DEV uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+  }
   // value held by lane 0 of the group
   static XHE_DEV uint32_t bcast0(uint32_t v) {
     if constexpr (TPI == 1) return v;
-    else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);
-    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x00, 0xF, 0xF, false);
+    else if constexpr (TPI == 2) return dpp<0xA0>(v);
+    else if constexpr (TPI == 4) return dpp<0x00>(v);
+    else return dpp<0x150>(v);
   }
   // value held by the last lane of the group
   static XHE_DEV uint32_t bcast_last(uint32_t v) {
     if constexpr (TPI == 1) return v;
-    else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF5, 0xF, 0xF, false);
-    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false);
+    else if constexpr (TPI == 2) return dpp<0xF5>(v);
+    else if constexpr (TPI == 4) return dpp<0xFF>(v);
+    else return dpp<0x15F>(v);
   }
   // value held by lane g+1 (0 for the last lane)
   static XHE_DEV uint32_t from_next(uint32_t v) {
     if constexpr (TPI == 1) return 0u;
+    else if constexpr (TPI == 16) return dpp<0x101>(v);  // lane 15 reads outside the row: 0
     else {
-      uint32_t r;
-      if constexpr (TPI == 2) r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF5, 0xF, 0xF, false);
-      else r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xF9, 0xF, 0xF, false);
+      uint32_t r = TPI == 2 ? dpp<0xF5>(v) : dpp<0xF9>(v);
       return g() == TPI - 1 ? 0u : r;
     }
   }
   // value held by lane g-1 (0 for lane 0)
   static XHE_DEV uint32_t from_prev(uint32_t v) {
     if constexpr (TPI == 1) return 0u;
+    else if constexpr (TPI == 16) return dpp<0x111>(v);  // lane 0 reads outside the row: 0
     else {
-      uint32_t r;
-      if constexpr (TPI == 2) r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xA0, 0xF, 0xF, false);
-      else r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x90, 0xF, 0xF, false);
+      uint32_t r = TPI == 2 ? dpp<0xA0>(v) : dpp<0x90>(v);
       return g() == 0 ? 0u : r;
     }
   }
@@ -453,13 +468,19 @@ struct Mont {
       // (the empty volatile asm pins each link between its barriers; plain
       // arithmetic would otherwise be sunk to its use at IR level)
       if (stage == 0) {
-        T[0] += lead ? (x0 >> W) : 0ull;
+        // every lane keeps the carry of the limb it hands down (position
+        // g*L-1 -> g*L is this lane's new T[0]); lane 0's limb is dropped
+        T[0] += x0 >> W;
         asm volatile("" : "+v"(T[0]));
       } else if (stage == 1) {
         xn = mad64(ai_next, b[0], T[0]);
         asm volatile("" : "+v"(xn));
       } else if (stage == 2) {
+#if XHE_M_MAD
+        t = (uint32_t)mad64((uint32_t)xn, n0inv, 0ull);
+#else
         t = (uint32_t)xn * n0inv;
+#endif
         asm volatile("" : "+v"(t));
       } else if (stage == 3) {
         mn = G::bcast0(t & MASK);
@@ -487,7 +508,7 @@ struct Mont {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (stage < 4) advance();
-    T[L - 1] = G::from_next64(x0);
+    T[L - 1] = (uint64_t)G::from_next((uint32_t)x0 & MASK);  // its carry stayed in lane g+1
     x0 = xn;
     m = mn;
   }
@@ -504,7 +525,35 @@ struct Mont {
       c = x >> W;
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (TPI > 1) {
+    if constexpr (TPI >= 4) {
+      // One round of lane-to-lane carries (c < 2^36 into L >= 5 limbs), after
+      // which every lane's carry-out is 0 or 1 and passes through a lane only
+      // when all its limbs are MASK: the remaining ripple is a carry-lookahead
+      // on the wave's lane masks (generate g, propagate p; carries into the
+      // lanes = (g + (g|p)) ^ g ^ (g|p)), with the group's top lane cleared so
+      // no carry crosses into the next group. TPI-1 ripple rounds -> 2 passes.
+      uint64_t cin = G::from_prev64(c);
+      uint32_t all = 1u;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        uint64_t x = (uint64_t)b[j] + cin;
+        b[j] = (uint32_t)x & MASK;
+        cin = x >> W;
+        all &= (b[j] == MASK) ? 1u : 0u;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      constexpr uint64_t top = TPI == 16 ? 0x8000800080008000ull : 0x8888888888888888ull;
+      const uint64_t gm = __builtin_amdgcn_ballot_w64(cin != 0) & ~top;
+      const uint64_t tm = (gm | __builtin_amdgcn_ballot_w64(all != 0)) & ~top;
+      const uint64_t cm = (gm + tm) ^ gm ^ tm;
+      uint32_t ci = (uint32_t)(cm >> (threadIdx.x & 63)) & 1u;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        uint32_t x = b[j] + ci;
+        b[j] = x & MASK;
+        ci = x >> W;
+      }
+    } else if constexpr (TPI > 1) {
 #pragma unroll
       for (int r = 1; r < TPI; ++r) {
         uint64_t cin = G::from_prev64(c);
@@ -752,17 +801,26 @@ struct Mont {
       b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
     }
   }
-  XHE_DEV void load_words(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
-    if constexpr (TPI == 1) {
-      load_words_g<0>(b, w, nwords);
+  template <int GG>
+  XHE_DEV void load_words_from(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords, int g) const {
+    if constexpr (GG == TPI - 1) {
+      load_words_g<GG>(b, w, nwords);
     } else {
-      switch (G::g()) {
-        case 0: load_words_g<0>(b, w, nwords); break;
-        case 1: load_words_g<1>(b, w, nwords); break;
-        case 2: if constexpr (TPI > 2) load_words_g<2>(b, w, nwords); break;
-        default: if constexpr (TPI > 2) load_words_g<TPI - 1>(b, w, nwords); break;
-      }
+      if (g == GG) load_words_g<GG>(b, w, nwords);
+      else load_words_from<GG + 1>(b, w, nwords, g);
     }
+  }
+  XHE_DEV void load_words(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) const {
+    load_words_from<0>(b, w, nwords, G::g());
+  }
+  // Store limbs [0, nlimbs) of the residue into an interleaved row (the
+  // residue's limbs beyond nlimbs must be zero).
+  XHE_DEV void store_strided_n(const uint32_t (&b)[L], uint32_t* p, int stride, int nlimbs) const {
+    p = opaque(p);
+    const int g = G::g();
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (g * L + j < nlimbs) p[(size_t)(g * L + j) * stride] = b[j];
   }
   // Store this lane's limbs one per word into an interleaved row.
   XHE_DEV void store_strided(const uint32_t (&b)[L], uint32_t* p, int stride) const {

@@ -41,13 +41,15 @@ struct HipError : std::runtime_error {
 // Limb shapes per key size: MP2 for residues mod p^2/q^2, MP for mod p/q.
 struct Shape2048 {
   using MP2 = Mont<74, 28, 1>;
-  using MP2L = Mont<76, 28, 4>;  // low-latency (small-batch) decrypt shape
+  using MP2L = Mont<76, 28, 4>;   // low-latency (small-batch) decrypt shape
+  using MP2X = Mont<80, 28, 16>;  // lowest latency: one 16-lane DPP row per residue (tiny batches)
   using MP = Mont<37, 28, 1>;
   using MN2 = Mont<152, 27, 4>;
 };
 struct Shape3072 {
   using MP2 = Mont<110, 28, 2>;
   using MP2L = Mont<112, 28, 4>;
+  using MP2X = Mont<112, 28, 16>;
   using MP = Mont<56, 28, 2>;
   using MN2 = Mont<228, 27, 4>;
 };
@@ -102,7 +104,7 @@ struct xhe_key {
   int K = 0, nw = 0, n2w = 0;
   bool priv = false, djn = false;
   int rand_bits = 0, rand_words = 0;
-  ModSpec mp2{}, mp{}, mn2{}, mp2L{};
+  ModSpec mp2{}, mp{}, mn2{}, mp2L{}, mp2X{};
   uint32_t* d_blob = nullptr;
   uint32_t* d_tab = nullptr;
   KeyDev kd{};
@@ -202,7 +204,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   k->rand_words = (k->rand_bits + 31) / 32;
 
   struct {
-    ModOff p2, q2, p, q, p2L, q2L;
+    ModOff p2, q2, p, q, p2L, q2L, p2X, q2X;
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
@@ -216,6 +218,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o.p2 = put_mod(bl, p2, s2);
     o.p2L = put_mod(bl, p2, k->mp2L);
     o.q2L = put_mod(bl, q2, k->mp2L);
+    o.p2X = put_mod(bl, p2, k->mp2X);
+    o.q2X = put_mod(bl, q2, k->mp2X);
     o.q2 = put_mod(bl, q2, s2);
     BigU R2p = pow2((size_t)s2.W * s2.S);
     BigU Rp2 = mod(R2p, p2), Rq2 = mod(R2p, q2);
@@ -287,6 +291,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.p2 = moddev(B, o.p2);
     kd.p2L = moddev(B, o.p2L);
     kd.q2L = moddev(B, o.q2L);
+    kd.p2X = moddev(B, o.p2X);
+    kd.q2X = moddev(B, o.q2X);
     kd.q2 = moddev(B, o.q2);
     kd.nR2_p2 = B + o.nR2_p2;
     kd.nR2_q2 = B + o.nR2_q2;
@@ -724,37 +730,58 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
   HIPCHK(hipFreeAsync(ws, s));
 }
 
-// Batches up to this size decrypt in the 4-lane shape (latency-bound regime:
-// fewer elements than wave slots x lanes / 2 primes).
-constexpr int64_t kDecLowLatMax = 16384;
+// Decrypt exponentiation shapes by batch size (latency- vs throughput-bound):
+// one 16-lane DPP row per residue up to kDecRowMax elements, 4 lanes up to
+// kDecQuadMax, one lane beyond (crossovers measured with tools/dec_shapes.py:
+// 16 lanes 6.0 ms flat to 1 k elements, 8.9 ms at 4 k, 15.8 ms at 8 k vs
+// 11.3/11.8/11.9 ms for 4 lanes; 4 lanes 20-21 ms at 16 k vs 36 ms for 1
+// lane, 40 ms at 32 k vs 37 ms). $XHE_DEC_TPI (1, 4 or 16) pins one shape.
+constexpr int64_t kDecRowMax = 5120;
+constexpr int64_t kDecQuadMax = 28672;
+
+int dec_tpi_override() {
+  static const int v = [] {
+    const char* e = std::getenv("XHE_DEC_TPI");
+    int t = e ? std::atoi(e) : 0;
+    return (t == 1 || t == 4 || t == 16) ? t : 0;
+  }();
+  return v;
+}
+
+template <class MP2S, int SHAPE, class MP2>
+void dec_pow_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chunk, uint32_t* xrows,
+                    hipStream_t s) {
+  int pow_blocks = (int)std::min<int64_t>((chunk * MP2S::TPI + 255) / 256, 512);
+  int64_t groups = (int64_t)pow_blocks * 256 / MP2S::TPI;
+  uint32_t* ws = nullptr;
+  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 17 * MP2S::S4 * groups * sizeof(uint32_t), s));
+  const ModDev& mp = SHAPE == 2 ? k->kd.p2X : SHAPE == 1 ? k->kd.p2L : k->kd.p2;
+  const ModDev& mq = SHAPE == 2 ? k->kd.q2X : SHAPE == 1 ? k->kd.q2L : k->kd.q2;
+  {
+    ProfScope ps("k_dec_pow", s);
+    hipLaunchKernelGGL((k_dec_pow<MP2S, SHAPE>), dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, mp.N, mq.N, ct, n,
+                       (int)MP2::S4, xrows, ws);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipFreeAsync(ws, s));
+}
 
 template <class Sh>
 void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
   using MP2 = typename Sh::MP2;
-  using MP2L = typename Sh::MP2L;
   using MP = typename Sh::MP;
-  static_assert(MP2L::S4 == MP2::S4, "x rows are shared by both decrypt shapes");
-  const bool lowlat = count <= kDecLowLatMax;
-  const int tpi = lowlat ? MP2L::TPI : MP2::TPI;
+  const int pin = dec_tpi_override();
+  const int tpi = pin ? pin : count <= kDecRowMax ? 16 : count <= kDecQuadMax ? 4 : 1;
   int64_t chunk = std::min<int64_t>(count, kChunk);
-  int pow_blocks = (int)std::min<int64_t>((chunk * tpi + 255) / 256, 512);
-  int64_t groups = (int64_t)pow_blocks * 256 / tpi;
-  uint32_t *ws = nullptr, *xrows = nullptr, *mrows = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 17 * MP2::S4 * groups * sizeof(uint32_t), s));
+  uint32_t *xrows = nullptr, *mrows = nullptr;
   HIPCHK(hipMallocAsync((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
   HIPCHK(hipMallocAsync((void**)&mrows, (size_t)2 * 2 * MP::S4 * chunk * sizeof(uint32_t), s));
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
-    {
-      ProfScope ps("k_dec_pow", s);
-      if (lowlat)
-        hipLaunchKernelGGL((k_dec_pow<MP2L, true>), dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2L.N,
-                           k->kd.q2L.N, ct + (size_t)off * k->n2w, n, xrows, ws);
-      else
-        hipLaunchKernelGGL(k_dec_pow<MP2>, dim3(pow_blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
-                           ct + (size_t)off * k->n2w, n, xrows, ws);
-      HIPCHK(hipGetLastError());
-    }
+    const uint32_t* cto = ct + (size_t)off * k->n2w;
+    if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
+    else if (tpi == 4) dec_pow_launch<typename Sh::MP2L, 1, MP2>(k, cto, n, chunk, xrows, s);
+    else dec_pow_launch<MP2, 0, MP2>(k, cto, n, chunk, xrows, s);
     int blocks = (int)((n * MP::TPI + 255) / 256);
     hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p.N, k->kd.q.N, n,
                        xrows, mrows);
@@ -763,7 +790,6 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
                        m + (size_t)off * k->nw);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
   HIPCHK(hipFreeAsync(xrows, s));
   HIPCHK(hipFreeAsync(mrows, s));
 }
@@ -855,11 +881,13 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     if (key_bits == 2048) {
       k->mp2 = {Shape2048::MP2::S, Shape2048::MP2::W};
       k->mp2L = {Shape2048::MP2L::S, Shape2048::MP2L::W};
+      k->mp2X = {Shape2048::MP2X::S, Shape2048::MP2X::W};
       k->mp = {Shape2048::MP::S, Shape2048::MP::W};
       k->mn2 = {Shape2048::MN2::S, Shape2048::MN2::W};
     } else {
       k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
       k->mp2L = {Shape3072::MP2L::S, Shape3072::MP2L::W};
+      k->mp2X = {Shape3072::MP2X::S, Shape3072::MP2X::W};
       k->mp = {Shape3072::MP::S, Shape3072::MP::W};
       k->mn2 = {Shape3072::MN2::S, Shape3072::MN2::W};
     }

@@ -40,6 +40,7 @@ struct KeyDev {
   // ---- mod p^2 / q^2 (shape MP2)
   ModDev p2, q2;
   ModDev p2L, q2L;            // the same moduli in the 4-lane decrypt shape (S = S4 of p2)
+  ModDev p2X, q2X;            // and in the 16-lane (one DPP row) decrypt shape
   const uint32_t* nR2_p2;     // n * R^2 mod p^2
   const uint32_t* nR2_q2;     // n * R^2 mod q^2
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
@@ -473,16 +474,20 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   }
 }
 
-// LOWLAT: the 4-lane shape (key.p2L/q2L) for small batches, where one lane
-// per residue leaves the chip idle and the 1,280 dependent products of one
-// element set the latency.
-template <class MP2, bool LOWLAT = false>
+// SHAPE 0: one lane per residue (key.p2/q2); 1: the 4-lane shape (p2L/q2L);
+// 2: the 16-lane shape (p2X/q2X). The wider shapes serve small batches, where
+// one lane per residue leaves the chip idle and the ~1,210 dependent products
+// of one element set the latency. x rows are written with the one-lane
+// shape's row count xs4 (limbs beyond it are zero), so k_dec_fin reads the
+// same layout whatever shape produced them.
+template <class MP2, int SHAPE = 0>
 __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* __restrict__ Np2,
                                                     const uint32_t* __restrict__ Nq2,
-                                                    const uint32_t* __restrict__ c_words, int64_t count,
+                                                    const uint32_t* __restrict__ c_words, int64_t count, int xs4,
                                                     uint32_t* __restrict__ xrows, uint32_t* __restrict__ ws) {
   const int prime = blockIdx.y;
-  const ModDev& md = LOWLAT ? (prime ? key.q2L : key.p2L) : (prime ? key.q2 : key.p2);
+  const ModDev& md = SHAPE == 2 ? (prime ? key.q2X : key.p2X)
+                     : SHAPE == 1 ? (prime ? key.q2L : key.p2L) : (prime ? key.q2 : key.p2);
   const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
   const int ebits = prime ? key.qm1_bits : key.pm1_bits;
   const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MP2::TPI;
@@ -528,7 +533,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
 #pragma unroll
     for (int j = 0; j < MP2::L; ++j) T[j] = (uint64_t)b[j] + (uint64_t)MP2::MASK;
     M.normalize(T, b);
-    M.store_strided(b, xrows + (size_t)prime * MP2::S4 * count + e, (int)count);
+    M.store_strided_n(b, xrows + (size_t)prime * xs4 * count + e, (int)count, xs4);
   }
 }
 
