@@ -1,0 +1,120 @@
+"""The n^2 ciphertext operations run in two lane shapes chosen by batch size
+(one 16-lane DPP row per residue up to 4,096 elements, 4 lanes beyond): add
+with exponent alignment, scalar powers (both signs), batch inversion,
+segmented products and multi-exponentiation give the same values in both
+shapes and match Python's pow arithmetic (the reference's gmpy2 semantics,
+utils.py:46-76) on sampled elements."""
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import FIXTURES, hx, load_fixture
+
+pytestmark = pytest.mark.gpu
+
+BIG, SMALL = 4200, 60  # 4-lane shape / 16-lane shape
+
+
+@pytest.fixture(scope="module", params=FIXTURES)
+def ctx(request):
+    from xfl_amd.paillier import PaillierContext
+    k = load_fixture(request.param)["key"]
+    return PaillierContext().init(hx(k["p"]), hx(k["q"])).to_public()
+
+
+def _rand_cts(ctx, n, seed):
+    rng = random.Random(seed)
+    return [rng.randrange(1, ctx.n_square) for _ in range(n)]
+
+
+def test_add_aligned_both_shapes(ctx):
+    from xfl_amd.paillier import ops
+    n2 = ctx.n_square
+    ra, rb = _rand_cts(ctx, BIG, 1), _rand_cts(ctx, BIG, 2)
+    rng = np.random.default_rng(3)
+    ea = rng.integers(-30, -20, BIG).astype(np.int32)
+    eb = rng.integers(-30, -20, BIG).astype(np.int32)
+    big, ebig = ops.add(ctx, ra, ea, rb, eb)
+    small, esmall = ops.add(ctx, ra[:SMALL], ea[:SMALL], rb[:SMALL], eb[:SMALL])
+    assert small == big[:SMALL] and list(esmall) == list(ebig[:SMALL])
+    for i in (0, 7, SMALL - 1, BIG - 1):
+        e = min(ea[i], eb[i])
+        want = pow(ra[i], 1 << int(ea[i] - e), n2) * pow(rb[i], 1 << int(eb[i] - e), n2) % n2
+        assert big[i] == want and ebig[i] == e
+
+
+@pytest.mark.parametrize("invert_first", [False, True])
+def test_powmod_both_shapes(ctx, invert_first):
+    from xfl_amd.paillier import ops
+    n2 = ctx.n_square
+    rs = _rand_cts(ctx, BIG, 4)
+    rng = random.Random(5)
+    ks = [rng.getrandbits(rng.choice([1, 20, 53, 75])) for _ in range(BIG)]
+    big = ops.powmod(ctx, rs, ks, invert_first=invert_first)
+    small = ops.powmod(ctx, rs[:SMALL], ks[:SMALL], invert_first=invert_first)
+    assert small == big[:SMALL]
+    for i in (0, 3, SMALL - 1, BIG - 1):
+        base = pow(rs[i], -1, n2) if invert_first else rs[i]
+        assert big[i] == pow(base, ks[i], n2)
+
+
+def test_segment_sums_both_shapes(ctx):
+    from xfl_amd.paillier import ops
+    n2 = ctx.n_square
+    for n in (BIG, SMALL):
+        rs = _rand_cts(ctx, n, 6)
+        exps = np.zeros(n, dtype=np.int64)
+        exps[::3] = -1
+        cuts = sorted(random.Random(7).sample(range(1, n), 9))
+        seg = np.array([0] + cuts + [n], dtype=np.int64)
+        got, emin = ops.segment_sums(ctx, rs, exps, seg)
+        for s in (0, 4, 9):
+            lo, hi = int(seg[s]), int(seg[s + 1])
+            want = 1
+            for i in range(lo, hi):
+                want = want * pow(rs[i], 1 << int(exps[i] - emin[s]), n2) % n2
+            assert got[s] == want
+
+
+@pytest.mark.parametrize("nbases,ncols", [(24, 5), (BIG + 100, 2)])
+def test_multiexp_both_shapes(ctx, nbases, ncols):
+    from xfl_amd.paillier import ops
+    n2 = ctx.n_square
+    bases = _rand_cts(ctx, nbases, 8)
+    rng = random.Random(9)
+    nterms = min(nbases, 40)
+    idx = [[rng.randrange(nbases) for _ in range(nterms)] for _ in range(ncols)]
+    ks = [[rng.getrandbits(60) for _ in range(nterms)] for _ in range(ncols)]
+    got = ops.multiexp(ctx, bases, idx, ks)
+    for j in range(ncols):
+        want = 1
+        for t in range(nterms):
+            want = want * pow(bases[idx[j][t]], ks[j][t], n2) % n2
+        assert got[j] == want
+
+
+def test_djn_encrypt_both_shapes():
+    """DJN private encryption: the 16-lane small-batch kernel (k_djn_pow_x, on
+    the one-lane tables with the (R'/R)^nwin start factor) and the one-lane
+    kernel give identical ciphertexts, equal to the closed form."""
+    from oracle import paillier_oracle as O
+    from xfl_amd._native import DeviceKey, ints_to_words, words_to_ints
+    for fx in FIXTURES:
+        g = load_fixture(fx)
+        k = g["key"]
+        if not k["djn_on"]:
+            continue
+        n, p, q, h = hx(k["n"]), hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
+        for win in (16, 7):
+            dk = DeviceKey(g["key_bits"], n, p, q, h, win_bits=win)
+            rng = random.Random(win)
+            ms = [rng.randrange(n) for _ in range(BIG)]
+            rs = [rng.randrange(1, 1 << dk.rand_bits) for _ in range(BIG)]
+            mw, rw = ints_to_words(ms, dk.nw), ints_to_words(rs, dk.rand_words)
+            big = words_to_ints(dk.encrypt_words(mw, rw))
+            small = words_to_ints(dk.encrypt_words(mw[:SMALL], rw[:SMALL]))
+            assert small == big[:SMALL]
+            ok = O.derive_private(p, q, h)
+            for i in (0, SMALL - 1, BIG - 1):
+                assert big[i] == O.encrypt_m(ok, ms[i], rs[i])

@@ -45,6 +45,7 @@ struct Shape2048 {
   using MP2X = Mont<80, 28, 16>;  // lowest latency: one 16-lane DPP row per residue (tiny batches)
   using MP = Mont<37, 28, 1>;
   using MN2 = Mont<152, 27, 4>;
+  using MN2X = Mont<160, 27, 16>;  // n^2 ops on small batches: one 16-lane DPP row per residue
 };
 struct Shape3072 {
   using MP2 = Mont<110, 28, 2>;
@@ -52,6 +53,7 @@ struct Shape3072 {
   using MP2X = Mont<112, 28, 16>;
   using MP = Mont<56, 28, 2>;
   using MN2 = Mont<228, 27, 4>;
+  using MN2X = Mont<240, 27, 16>;
 };
 
 struct ModSpec {
@@ -104,7 +106,7 @@ struct xhe_key {
   int K = 0, nw = 0, n2w = 0;
   bool priv = false, djn = false;
   int rand_bits = 0, rand_words = 0;
-  ModSpec mp2{}, mp{}, mn2{}, mp2L{}, mp2X{};
+  ModSpec mp2{}, mp{}, mn2{}, mp2L{}, mp2X{}, mn2X{};
   uint32_t* d_blob = nullptr;
   uint32_t* d_tab = nullptr;
   KeyDev kd{};
@@ -193,6 +195,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   size_t o_minneg = bl.put_words(minneg, k->nw);
   size_t o_nlim = bl.put_limbs(n, k->mp2);
   ModOff o_n2m = put_mod(bl, n2, k->mn2);
+  ModOff o_n2X = put_mod(bl, n2, k->mn2X);
   size_t o_nR2n2, o_hMn2 = 0;
   {
     BigU Rn2 = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
@@ -205,6 +208,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
 
   struct {
     ModOff p2, q2, p, q, p2L, q2L, p2X, q2X;
+    size_t nR2C_p2X = 0, nR2C_q2X = 0, R1C_p2X = 0, R1C_q2X = 0;
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
@@ -234,6 +238,19 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     if (k->djn) {
       o.hM_p2 = bl.put_limbs(mulmod(mod(*h, p2), Rp2, p2), s2);  // h_pow_n mod p^2 (context.py:63)
       o.hM_q2 = bl.put_limbs(mulmod(mod(*h, q2), Rq2, q2), s2);
+      // 16-lane small-batch shape on the same tables (k_djn_pow_x)
+      const int nwin = (k->rand_bits + win - 1) / win;
+      const ModSpec& sx = k->mp2X;
+      BigU Rx = pow2((size_t)sx.W * sx.S);
+      BigU Cexp = pow2((size_t)(sx.S - s2.S) * s2.W * nwin);  // (R'/R)^nwin
+      auto put_x = [&](const BigU& P2, size_t* nr2c, size_t* r1c) {
+        BigU C = mod(Cexp, P2), RxP = mod(Rx, P2);
+        BigU CR = mulmod(C, RxP, P2);
+        *r1c = bl.put_limbs(CR, sx);
+        *nr2c = bl.put_limbs(mulmod(mod(n, P2), mulmod(CR, RxP, P2), P2), sx);
+      };
+      put_x(p2, &o.nR2C_p2X, &o.R1C_p2X);
+      put_x(q2, &o.nR2C_q2X, &o.R1C_q2X);
     }
     // mod p / q (decrypt)
     o.p = put_mod(bl, P, s1);
@@ -285,6 +302,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   kd.minneg = B + o_minneg;
   kd.n_lim = B + o_nlim;
   kd.n2 = moddev(B, o_n2m);
+  kd.n2X = moddev(B, o_n2X);
   kd.nR2_n2 = B + o_nR2n2;
   kd.n_bits = (int)n.bits();
   if (k->priv) {
@@ -295,6 +313,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.q2X = moddev(B, o.q2X);
     kd.q2 = moddev(B, o.q2);
     kd.nR2_p2 = B + o.nR2_p2;
+    kd.nR2C_p2X = B + o.nR2C_p2X;
+    kd.nR2C_q2X = B + o.nR2C_q2X;
+    kd.R1C_p2X = B + o.R1C_p2X;
+    kd.R1C_q2X = B + o.R1C_q2X;
     kd.nR2_q2 = B + o.nR2_q2;
     kd.q2invR_p2 = B + o.q2invR;
     kd.q2_lim = B + o.q2_lim;
@@ -388,6 +410,19 @@ struct ProfScope {
   }
 };
 
+// DJN private encryption in the 16-lane shape up to kEncRowMax elements
+// (tools/dec_shapes.py --enc: 64 elements 0.50 ms vs 1.95 ms one lane per
+// residue, 16 k 1.86 vs 2.16 ms, 64 k 6.2 vs 3.8 ms); $XHE_ENC_TPI (16 or 0)
+// pins it.
+constexpr int64_t kEncRowMax = 20480;
+bool enc_row(int64_t count) {
+  static const int pin = [] {
+    const char* e = std::getenv("XHE_ENC_TPI");
+    return e ? std::atoi(e) : -1;
+  }();
+  return pin >= 0 ? pin == 16 : count <= kEncRowMax;
+}
+
 template <class Sh>
 void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -397,7 +432,13 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
-    {
+    if (enc_row(n)) {
+      // small batch: one 16-lane DPP row per residue (latency-bound regime)
+      using MX = typename Sh::MP2X;
+      hipLaunchKernelGGL((k_djn_pow_x<MX, MP2::S4>), dim3((unsigned)((n * MX::TPI + 255) / 256), 2), dim3(256), 0, s,
+                         k->kd, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, ws);
+      HIPCHK(hipGetLastError());
+    } else {
       ProfScope ps("k_djn_pow", s);
 #if XHE_LDS_ROWS
       if constexpr (MP2::TPI == 1) {
@@ -486,17 +527,37 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
   }
 }
 
-template <class Sh>
+// n^2 constants of the MN2 shape (see n2dev in xhe_kernels.hpp).
+template <class MN2>
+const ModDev& n2h(const xhe_key* k) {
+  if constexpr (MN2::TPI == 16) return k->kd.n2X;
+  else return k->kd.n2;
+}
+
+// Shape of the n^2 ciphertext ops by batch size: one 16-lane DPP row per
+// residue up to kN2RowMax elements (latency-bound: a few ciphertexts leave the
+// chip idle and each element's chain of dependent products sets the time),
+// 4 lanes beyond. $XHE_N2_TPI (4 or 16) pins one shape (A/B measurement).
+constexpr int64_t kN2RowMax = 4096;
+bool n2_row(int64_t count) {
+  static const int pin = [] {
+    const char* e = std::getenv("XHE_N2_TPI");
+    int t = e ? std::atoi(e) : 0;
+    return (t == 4 || t == 16) ? t : 0;
+  }();
+  return pin ? pin == 16 : count <= kN2RowMax;
+}
+
+template <class Sh, class MN2 = typename Sh::MN2>
 void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
                  int64_t count, int dmax, uint32_t* out, int32_t* eout, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
   HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * MN2::S4 * chunk * sizeof(uint32_t), s));
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MN2::TPI + 255) / 256);
-    hipLaunchKernelGGL(k_mulmod_n2<MN2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.n2.N, a + (size_t)off * k->n2w,
+    hipLaunchKernelGGL(k_mulmod_n2<MN2>, dim3(blocks), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, a + (size_t)off * k->n2w,
                        ea ? ea + off : nullptr, b + (size_t)off * k->n2w, eb ? eb + off : nullptr, n, dmax,
                        out + (size_t)off * k->n2w, eout ? eout + off : nullptr, ws);
     HIPCHK(hipGetLastError());
@@ -504,10 +565,9 @@ void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const u
   HIPCHK(hipFreeAsync(ws, s));
 }
 
-template <class Sh>
+template <class Sh, class MN2 = typename Sh::MN2>
 void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int kw, int kbits, int64_t count,
                  uint32_t* out, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   int pb = pow_grid<MN2>(chunk, 512);
   int64_t groups = (int64_t)pb * 256 / MN2::TPI;
@@ -516,7 +576,7 @@ void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int k
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     ProfScope ps("k_powmod_n2", s);
-    hipLaunchKernelGGL(k_powmod_n2<MN2>, dim3(pb), dim3(256), 0, s, k->kd, k->kd.n2.N, c + (size_t)off * k->n2w,
+    hipLaunchKernelGGL(k_powmod_n2<MN2>, dim3(pb), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, c + (size_t)off * k->n2w,
                        kw_ + (size_t)off * kw, kw, kbits, n, out + (size_t)off * k->n2w, ws);
     HIPCHK(hipGetLastError());
   }
@@ -524,9 +584,8 @@ void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int k
 }
 
 // Batch inversion mod n^2 via a product tree (Montgomery's trick in parallel).
-template <class Sh>
+template <class Sh, class MN2 = typename Sh::MN2>
 int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* out, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   const int S4 = MN2::S4;
   std::vector<int64_t> sizes{count};
   while (sizes.back() > 1) sizes.push_back((sizes.back() + 1) / 2);
@@ -543,17 +602,17 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   HIPCHK(hipMallocAsync((void**)&scr, (size_t)(4 * (k->n2w + 1) + 2 * k->n2w + 8) * 4, s));
   HIPCHK(hipMallocAsync((void**)&st, 4, s));
   auto blocks = [&](int64_t n) { return dim3((unsigned)((n * MN2::TPI + 255) / 256)); };
-  hipLaunchKernelGGL(k_to_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, count, lv);
+  hipLaunchKernelGGL(k_to_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, c, count, lv);
   HIPCHK(hipGetLastError());
   for (size_t l = 1; l < sizes.size(); ++l) {
-    hipLaunchKernelGGL(k_tree_up<MN2>, blocks(sizes[l]), dim3(256), 0, s, k->kd, k->kd.n2.N, lv + offs[l - 1],
+    hipLaunchKernelGGL(k_tree_up<MN2>, blocks(sizes[l]), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, lv + offs[l - 1],
                        sizes[l - 1], lv + offs[l], sizes[l]);
     HIPCHK(hipGetLastError());
   }
   size_t top = offs.back();
   uint32_t* y_words = scr + 4 * (k->n2w + 1);
   uint32_t* r_words = y_words + k->n2w;
-  hipLaunchKernelGGL(k_row_pack<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, lv + top, r_words);
+  hipLaunchKernelGGL(k_row_pack<MN2>, dim3(1), dim3(64), 0, s, k->kd, n2h<MN2>(k).N, lv + top, r_words);
   HIPCHK(hipGetLastError());
   // The one scalar inverse of the batch (the tree root, (prod c_i) R) is a
   // sequential extended Euclid: ~1 ms on a host core vs a single GPU lane's
@@ -569,14 +628,14 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
     return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
   }
   HIPCHK(hipMemcpyAsync(y_words, yinv.data(), (size_t)k->n2w * 4, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_inv_to_row<MN2>, dim3(1), dim3(64), 0, s, k->kd, k->kd.n2.N, y_words, inv + top);
+  hipLaunchKernelGGL(k_inv_to_row<MN2>, dim3(1), dim3(64), 0, s, k->kd, n2h<MN2>(k).N, y_words, inv + top);
   HIPCHK(hipGetLastError());
   for (size_t l = sizes.size() - 1; l >= 1; --l) {
-    hipLaunchKernelGGL(k_tree_down<MN2>, blocks(sizes[l - 1]), dim3(256), 0, s, k->kd, k->kd.n2.N, inv + offs[l],
+    hipLaunchKernelGGL(k_tree_down<MN2>, blocks(sizes[l - 1]), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, inv + offs[l],
                        sizes[l], lv + offs[l - 1], sizes[l - 1], inv + offs[l - 1]);
     HIPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, inv, count, out);
+  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(count), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, inv, count, out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(lv);
@@ -590,9 +649,8 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
 // (seg: nseg+1 offsets) by levels of k_chunk_prod (C rows per chunk). Takes
 // ownership of `rows`; returns a new [S4][nseg] buffer (hipFree by the
 // caller); an empty segment yields the Montgomery one.
-template <class Sh>
+template <class Sh, class MN2 = typename Sh::MN2>
 uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   const int S4 = MN2::S4;
   const int64_t C = 32;  // chunk length per level
   const int64_t nseg = (int64_t)seg.size() - 1;
@@ -617,7 +675,7 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
     HIPCHK(hipMallocAsync((void**)&dcb, cb.size() * 8, s));
     HIPCHK(hipMemcpyAsync(dcb, cb.data(), cb.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(n_out, 1) * 4, s));
-    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, k->kd.n2.N, cur, n_cur, dcb, n_out,
+    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, n_cur, dcb, n_out,
                        nxt);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));  // cb lives on the host stack
@@ -633,22 +691,21 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
 
 // Segmented modular product: out[s] = prod_{i in seg s} c_i^(2^d_i) mod n^2.
 // seg_begin: nseg+1 offsets into the (already segment-ordered) inputs.
-template <class Sh>
+template <class Sh, class MN2 = typename Sh::MN2>
 void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dmax, int64_t count,
                   const int64_t* seg_begin_host, int64_t nseg, uint32_t* out, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   const int S4 = MN2::S4;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
   uint32_t *rows = nullptr, *sq = nullptr;
   HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
   HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
   if (count > 0) {
-    hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, k->kd.n2.N, c, d, count, dmax,
+    hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, c, d, count, dmax,
                        rows, sq);
     HIPCHK(hipGetLastError());
   }
-  uint32_t* cur = reduce_segments<Sh>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s);
-  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, k->kd.n2.N, cur, nseg, out);
+  uint32_t* cur = reduce_segments<Sh, MN2>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s);
+  hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, nseg, out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(cur);
@@ -674,10 +731,9 @@ int mexp_window(int64_t nbases, int64_t ncols, int64_t nterms, int kbits, int s4
 }
 
 // Multi-exponentiation out[j] = prod_t bases[idx[j][t]]^k[j][t] mod n^2.
-template <class Sh>
+template <class Sh, class MN2 = typename Sh::MN2>
 void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* kx,
                    int kw, int kbits, int64_t ncols, int64_t nterms, int c, uint32_t* out, hipStream_t s) {
-  using MN2 = typename Sh::MN2;
   const int S4 = MN2::S4;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
   const int nwin = std::max(1, (kbits + c - 1) / c);
@@ -685,27 +741,27 @@ void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, cons
   HIPCHK(hipMallocAsync((void**)&tab, ((size_t)nbases << c) * S4 * 4, s));
   {
     ProfScope ps("k_mexp_tab", s);
-    hipLaunchKernelGGL(k_mexp_tab<MN2>, blocks(nbases), dim3(256), 0, s, k->kd, k->kd.n2.N, bases, nbases, c, tab);
+    hipLaunchKernelGGL(k_mexp_tab<MN2>, blocks(nbases), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, bases, nbases, c, tab);
     HIPCHK(hipGetLastError());
   }
   // enough lane groups to fill the chip, at least 2 terms per group
   const int64_t segs = ncols * nwin;
-  const int64_t target_groups = 32768;
+  const int64_t target_groups = 131072 / MN2::TPI;
   const int64_t chunk = std::max<int64_t>(2, std::min<int64_t>(64, (segs * nterms + target_groups - 1) / target_groups));
   const int64_t nchunks = (nterms + chunk - 1) / chunk;
   const int64_t n_out = segs * nchunks;
   HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * n_out * 4, s));
   {
     ProfScope ps("k_mexp_gather", s);
-    hipLaunchKernelGGL(k_mexp_gather<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, k->kd.n2.N, tab, c, idx, kx, kw,
+    hipLaunchKernelGGL(k_mexp_gather<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, tab, c, idx, kx, kw,
                        nterms, nwin, nchunks, chunk, n_out, rows);
     HIPCHK(hipGetLastError());
   }
   std::vector<int64_t> seg(segs + 1);
   for (int64_t i = 0; i <= segs; ++i) seg[i] = i * nchunks;
-  uint32_t* P = reduce_segments<Sh>(k, rows, n_out, std::move(seg), s);
+  uint32_t* P = reduce_segments<Sh, MN2>(k, rows, n_out, std::move(seg), s);
   HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * ncols * 4, s));
-  hipLaunchKernelGGL(k_mexp_horner<MN2>, blocks(ncols), dim3(256), 0, s, k->kd, k->kd.n2.N, P, nwin, c, ncols, sq,
+  hipLaunchKernelGGL(k_mexp_horner<MN2>, blocks(ncols), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, P, nwin, c, ncols, sq,
                      out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
@@ -816,8 +872,15 @@ int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev,
     for (int64_t i = 0; i < nseg; ++i)
       if (seg_begin[i + 1] < seg_begin[i]) return fail(XHE_EINVAL, "xhe_segprod: offsets must be non-decreasing");
     DevGuard dg(key->device);
-    if (key->K == 2048) segprod_impl<Shape2048>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, (hipStream_t)stream);
-    else segprod_impl<Shape3072>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, (hipStream_t)stream);
+    const bool row = n2_row(count);
+    hipStream_t hs = (hipStream_t)stream;
+    if (key->K == 2048) {
+      if (row) segprod_impl<Shape2048, Shape2048::MN2X>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+      else segprod_impl<Shape2048>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+    } else {
+      if (row) segprod_impl<Shape3072, Shape3072::MN2X>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+      else segprod_impl<Shape3072>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+    }
     return XHE_OK;
   });
 }
@@ -884,12 +947,14 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
       k->mp2X = {Shape2048::MP2X::S, Shape2048::MP2X::W};
       k->mp = {Shape2048::MP::S, Shape2048::MP::W};
       k->mn2 = {Shape2048::MN2::S, Shape2048::MN2::W};
+      k->mn2X = {Shape2048::MN2X::S, Shape2048::MN2X::W};
     } else {
       k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
       k->mp2L = {Shape3072::MP2L::S, Shape3072::MP2L::W};
       k->mp2X = {Shape3072::MP2X::S, Shape3072::MP2X::W};
       k->mp = {Shape3072::MP::S, Shape3072::MP::W};
       k->mn2 = {Shape3072::MN2::S, Shape3072::MN2::W};
+      k->mn2X = {Shape3072::MN2X::S, Shape3072::MN2X::W};
     }
     BigU n = BigU::from_words(n_words, k->nw);
     if ((int)n.bits() > key_bits || n.bits() + 2 < (size_t)key_bits)
@@ -1066,8 +1131,15 @@ int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev,
       return fail(XHE_EINVAL, "xhe_mulmod: bad argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    if (key->K == 2048) mulmod_impl<Shape2048>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, (hipStream_t)stream);
-    else mulmod_impl<Shape3072>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, (hipStream_t)stream);
+    const bool row = n2_row(count);
+    hipStream_t hs = (hipStream_t)stream;
+    if (key->K == 2048) {
+      if (row) mulmod_impl<Shape2048, Shape2048::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+      else mulmod_impl<Shape2048>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+    } else {
+      if (row) mulmod_impl<Shape3072, Shape3072::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+      else mulmod_impl<Shape3072>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+    }
     return XHE_OK;
   });
 }
@@ -1079,8 +1151,15 @@ int xhe_powmod(const xhe_key* key, const uint32_t* c_dev, const uint32_t* k_dev,
       return fail(XHE_EINVAL, "xhe_powmod: bad argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    if (key->K == 2048) powmod_impl<Shape2048>(key, c_dev, k_dev, kw, kbits, count, out_dev, (hipStream_t)stream);
-    else powmod_impl<Shape3072>(key, c_dev, k_dev, kw, kbits, count, out_dev, (hipStream_t)stream);
+    const bool row = n2_row(count);
+    hipStream_t hs = (hipStream_t)stream;
+    if (key->K == 2048) {
+      if (row) powmod_impl<Shape2048, Shape2048::MN2X>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+      else powmod_impl<Shape2048>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+    } else {
+      if (row) powmod_impl<Shape3072, Shape3072::MN2X>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+      else powmod_impl<Shape3072>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+    }
     return XHE_OK;
   });
 }
@@ -1090,8 +1169,13 @@ int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_
     if (!key || (count > 0 && (!c_dev || !out_dev))) return fail(XHE_EINVAL, "xhe_invert: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    if (key->K == 2048) return invert_impl<Shape2048>(key, c_dev, count, out_dev, (hipStream_t)stream);
-    return invert_impl<Shape3072>(key, c_dev, count, out_dev, (hipStream_t)stream);
+    const bool row = n2_row(count);
+    hipStream_t hs = (hipStream_t)stream;
+    if (key->K == 2048)
+      return row ? invert_impl<Shape2048, Shape2048::MN2X>(key, c_dev, count, out_dev, hs)
+                 : invert_impl<Shape2048>(key, c_dev, count, out_dev, hs);
+    return row ? invert_impl<Shape3072, Shape3072::MN2X>(key, c_dev, count, out_dev, hs)
+               : invert_impl<Shape3072>(key, c_dev, count, out_dev, hs);
   });
 }
 
@@ -1278,14 +1362,25 @@ int xhe_multiexp(const xhe_key* key, const uint32_t* bases_dev, int64_t nbases, 
     if (ncols * nterms > (int64_t)1 << 31 || nbases > (int64_t)1 << 30)
       return fail(XHE_EINVAL, "xhe_multiexp: problem too large for one call");
     DevGuard dg(key->device);
-    const int s4 = key->K == 2048 ? Shape2048::MN2::S4 : Shape3072::MN2::S4;
+    const bool row = n2_row(std::max(nbases, ncols));
+    const int s4 = key->K == 2048 ? (row ? Shape2048::MN2X::S4 : Shape2048::MN2::S4)
+                                  : (row ? Shape3072::MN2X::S4 : Shape3072::MN2::S4);
     const int c = win_bits ? win_bits : mexp_window(nbases, ncols, nterms, std::max(kbits, 1), s4);
-    if (key->K == 2048)
-      multiexp_impl<Shape2048>(key, bases_dev, nbases, idx_dev, k_dev, kw, std::max(kbits, 1), ncols, nterms, c,
-                               out_dev, (hipStream_t)stream);
-    else
-      multiexp_impl<Shape3072>(key, bases_dev, nbases, idx_dev, k_dev, kw, std::max(kbits, 1), ncols, nterms, c,
-                               out_dev, (hipStream_t)stream);
+    const int kb = std::max(kbits, 1);
+    hipStream_t hs = (hipStream_t)stream;
+    if (key->K == 2048) {
+      if (row)
+        multiexp_impl<Shape2048, Shape2048::MN2X>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c,
+                                                  out_dev, hs);
+      else
+        multiexp_impl<Shape2048>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev, hs);
+    } else {
+      if (row)
+        multiexp_impl<Shape3072, Shape3072::MN2X>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c,
+                                                  out_dev, hs);
+      else
+        multiexp_impl<Shape3072>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev, hs);
+    }
     return XHE_OK;
   });
 }

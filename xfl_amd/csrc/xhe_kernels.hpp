@@ -41,7 +41,12 @@ struct KeyDev {
   ModDev p2, q2;
   ModDev p2L, q2L;            // the same moduli in the 4-lane decrypt shape (S = S4 of p2)
   ModDev p2X, q2X;            // and in the 16-lane (one DPP row) decrypt shape
+  ModDev n2X;                 // n^2 in the 16-lane shape (small-batch ciphertext ops)
   const uint32_t* nR2_p2;     // n * R^2 mod p^2
+  // 16-lane (p2X/q2X, R' = 2^(W*80)) DJN shape on the one-lane tables: every
+  // table product scales by R/R', so the start value carries C = (R'/R)^nwin:
+  const uint32_t *nR2C_p2X, *nR2C_q2X;  // n * C * R'^2 mod P^2
+  const uint32_t *R1C_p2X, *R1C_q2X;    // C * R' mod P^2
   const uint32_t* nR2_q2;     // n * R^2 mod q^2
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
   const uint32_t* q2_lim;     // q^2 (MP2 limbs)
@@ -265,6 +270,48 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   M.mul(b, AOne{});
   M.reduce_once(b);
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+}
+
+// A table row of RS4 words read by a wider-shape Montgomery product (limbs
+// beyond the row are zero).
+template <int RS4>
+struct ARowZ {
+  const uint32_t* __restrict__ p;
+  XHE_DEV uint4 load4(int i) const {
+    return i < RS4 ? *reinterpret_cast<const uint4*>(p + i) : make_uint4(0u, 0u, 0u, 0u);
+  }
+};
+
+// k_djn_pow for small batches: one 16-lane DPP row per residue (key.p2X/q2X)
+// on the same one-lane tables (rows of RS4 words, Montgomery factor R): with
+// the start value (1 + n m) C R', C = (R'/R)^nwin, the nwin table products
+// leave (1 + n m) h^a R' exactly as the one-lane kernel leaves (1 + n m) h^a R.
+// Output rows as k_djn_pow (RS4 limbs, stride count) for k_crt_enc.
+template <class MX, int RS4>
+__global__ void __launch_bounds__(256, 2) k_djn_pow_x(KeyDev key, const uint32_t* __restrict__ m_words,
+                                                      const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                      uint32_t* __restrict__ ws) {
+  static_assert(MX::TPI == 16, "16-lane shape");
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MX::TPI;
+  if (e >= count) return;
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2X : key.p2X;
+  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
+  MX M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MX::L];
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{prime ? key.nR2C_q2X : key.nR2C_p2X});  // n m C R'
+  M.add_row(b, prime ? key.R1C_q2X : key.R1C_p2X);     // (1 + n m) C R'
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  const int rows = 1 << key.win;
+  for (int w = 0; w < key.nwin; ++w) {
+    uint32_t d = digit_at(ae, aw, w * key.win, key.win);
+    M.mul(b, ARowZ<RS4>{tab + ((size_t)w * rows + d) * RS4});
+  }
+  M.mul(b, AOne{});
+  M.reduce_once(b);
+  M.store_strided_n(b, ws + (size_t)prime * 2 * RS4 * count + e, (int)count, RS4);
 }
 
 #if XHE_LDS_ROWS
@@ -658,6 +705,14 @@ XHE_DEV uint32_t nibble(const uint32_t* w, int nwords, int win) {
 // out = a * b mod n^2 after aligning exponents: the operand with the larger
 // exponent is raised to 2^(e - min(ea, eb)) first (paillier.py:79-86,106-123).
 // ws: 2 rows [2*S4][count] per element (second row = pack scratch).
+// n^2 constants in the shape of MN2: the 4-lane shape (key.n2) or the
+// 16-lane one (key.n2X, small batches).
+template <class MN2>
+XHE_DEV const ModDev& n2dev(const KeyDev& key) {
+  if constexpr (MN2::TPI == 16) return key.n2X;
+  else return key.n2;
+}
+
 template <class MN2>
 __global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t* __restrict__ Nn2,
                                                       const uint32_t* __restrict__ a, const int32_t* __restrict__ ea,
@@ -670,14 +725,14 @@ __global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t
   uint32_t* row = ws + e;
   uint32_t* sq = ws + (size_t)MN2::S4 * count + e;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   const int e1 = ea ? ea[e] : 0, e2 = eb ? eb[e] : 0;
   const int emin = e1 < e2 ? e1 : e2;
   const int d1 = e1 - emin, d2 = e2 - emin;
   uint32_t b[MN2::L];
   // A = a R, squared d1 times, parked in `row`
   M.load_words(b, a + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{key.n2.R2});
+  M.mul(b, ARow{n2dev<MN2>(key).R2});
   for (int k = 0; k < dmax; ++k) {
     if (k < d1) {
       M.store_strided(b, sq, st);
@@ -687,7 +742,7 @@ __global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t
   }
   M.store_strided(b, row, st);
   M.load_words(b, bw + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{key.n2.R2});
+  M.mul(b, ARow{n2dev<MN2>(key).R2});
   for (int k = 0; k < dmax; ++k) {
     if (k < d2) {
       M.store_strided(b, sq, st);
@@ -725,12 +780,12 @@ __global__ void __launch_bounds__(256, 2) k_powmod_n2(KeyDev key, const uint32_t
 #endif
   for (int64_t e = gid0; e < count; e += G_total) {
     MN2 M;
-    M.init(Nn2, key.n2.n0inv);
+    M.init(Nn2, n2dev<MN2>(key).n0inv);
     uint32_t b[MN2::L];
     M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
-    M.mul(b, ARow{key.n2.R2});
+    M.mul(b, ARow{n2dev<MN2>(key).R2});
     const uint32_t* ke = k + (size_t)e * kw;
-    pow_window4(M, b, key.n2.R1, nwin, [&](int w) { return nibble(ke, kw, w); }, tab, sq, st, sq_lds);
+    pow_window4(M, b, n2dev<MN2>(key).R1, nwin, [&](int w) { return nibble(ke, kw, w); }, tab, sq, st, sq_lds);
     M.mul(b, AOne{});
     M.reduce_once(b);
     store_packed(M, b, sq, st, out + (size_t)e * key.n2w, key.n2w);
@@ -856,10 +911,10 @@ __global__ void __launch_bounds__(256, 2) k_align_mont(KeyDev key, const uint32_
   if (e >= count) return;
   const int st = (int)count;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{key.n2.R2});
+  M.mul(b, ARow{n2dev<MN2>(key).R2});
   const int de = d ? d[e] : 0;
   for (int k = 0; k < dmax; ++k) {
     if (k < de) {
@@ -882,11 +937,11 @@ __global__ void __launch_bounds__(256, 2) k_chunk_prod(KeyDev key, const uint32_
   const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (j >= n_out) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   const int64_t lo = cbeg[j], hi = cbeg[j + 1];
   if (hi <= lo) {  // empty segment: Montgomery one
-    M.load_row(b, key.n2.R1);
+    M.load_row(b, n2dev<MN2>(key).R1);
     M.reduce_once(b);
   } else {
     M.load_strided(b, in + lo, (int)n_in);
@@ -905,7 +960,7 @@ __global__ void __launch_bounds__(256, 2) k_tree_up(KeyDev key, const uint32_t* 
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (i >= n_out) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_strided(b, in + 2 * i, (int)n_in);
   if (2 * i + 1 < n_in) {
@@ -924,7 +979,7 @@ __global__ void __launch_bounds__(256, 2) k_tree_down(KeyDev key, const uint32_t
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (i >= n_child) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_strided(b, pinv + i / 2, (int)n_par);
   const int64_t sib = i ^ 1;
@@ -943,10 +998,10 @@ __global__ void __launch_bounds__(256, 2) k_to_mont_rows(KeyDev key, const uint3
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (e >= count) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{key.n2.R2});
+  M.mul(b, ARow{n2dev<MN2>(key).R2});
   M.reduce_once(b);
   M.store_strided(b, rows + e, (int)count);
 }
@@ -958,7 +1013,7 @@ __global__ void __launch_bounds__(256, 2) k_from_mont_rows(KeyDev key, const uin
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (e >= count) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_strided(b, rows + e, (int)count);
   M.mul(b, AOne{});
@@ -979,10 +1034,10 @@ __global__ void k_inv_to_row(KeyDev key, const uint32_t* __restrict__ Nn2, const
                              uint32_t* __restrict__ row) {
   if (blockIdx.x != 0 || threadIdx.x >= MN2::TPI) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_words(b, y, key.n2w);
-  M.mul(b, ARow{key.n2.R3});
+  M.mul(b, ARow{n2dev<MN2>(key).R3});
   M.reduce_once(b);
   M.store_row(b, row);
 }
@@ -1001,14 +1056,14 @@ __global__ void __launch_bounds__(256, 2) k_mexp_tab(KeyDev key, const uint32_t*
   const int64_t bi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (bi >= nbases) return;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t* t = tab + ((size_t)bi << c) * MN2::S4;
   uint32_t b[MN2::L];
-  M.load_row(b, key.n2.R1);
+  M.load_row(b, n2dev<MN2>(key).R1);
   M.reduce_once(b);
   M.store_row(b, t);  // base^0 = R
   M.load_words(b, bases + (size_t)bi * key.n2w, key.n2w);
-  M.mul(b, ARow{key.n2.R2});
+  M.mul(b, ARow{n2dev<MN2>(key).R2});
   M.reduce_once(b);
   M.store_row(b, t + MN2::S4);
   wave_sync_mem_();
@@ -1037,7 +1092,7 @@ __global__ void __launch_bounds__(256, 2) k_mexp_gather(KeyDev key, const uint32
   const int w = (int)(s - j * nwin);
   const int64_t lo = t * chunk, hi = lo + chunk < nterms ? lo + chunk : nterms;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   const int32_t* ij = idx + j * nterms;
   const uint32_t* kj = kx + (size_t)j * nterms * kw;
@@ -1063,7 +1118,7 @@ __global__ void __launch_bounds__(256, 2) k_mexp_horner(KeyDev key, const uint32
   const int pst = (int)(ncols * nwin);
   const int st = (int)ncols;
   MN2 M;
-  M.init(Nn2, key.n2.n0inv);
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_strided(b, P + j * nwin + (nwin - 1), pst);
   for (int w = nwin - 2; w >= 0; --w) {

@@ -195,6 +195,33 @@ def _div(a, b):
     return _mul(a, np.vectorize(lambda s: 1 / s, otypes=[object])(B))
 
 
+def _encode_scalars_vec(X):
+    """Vectorised PaillierEncoder.cal_exponent(precision=None) + encode_single
+    (encoder.py:29-54) of a plain numeric matrix, as (|k|, k negative, e):
+    floats give e = frexp exponent - 53 and |k| = |mantissa| * 2^53 (exact),
+    ints e = 0 and |k| = |x|; a negative value encodes to n - |k|, which is
+    >= min_value_for_negative for every |k| < 2^63 (the _raw_mul negative
+    branch, paillier.py:178-184). None outside the domain where that holds
+    without the reference's range errors (non-finite, |x| >= 2^53, |x| below
+    2^-960): the caller then runs the scalar encoder element by element."""
+    if X.dtype.kind == "f":
+        x = X.astype(np.float64)
+        ax = np.abs(x)
+        if not np.all(np.isfinite(x)) or np.any(ax >= 2.0 ** 53) or np.any((ax < 2.0 ** -960) & (ax != 0)):
+            return None
+        mant, expo = np.frexp(x)
+        kabs = (np.abs(mant) * 2.0 ** 53).astype(np.int64)
+        return kabs, x < 0, expo.astype(np.int64) - 53
+    if X.dtype.kind in "iu" and X.dtype.itemsize <= 8:
+        if X.dtype.kind == "u" and X.size and int(X.max()) >= 2 ** 63:
+            return None
+        x = X.astype(np.int64)
+        if X.dtype.kind == "i" and np.any(x == np.iinfo(np.int64).min):
+            return None
+        return np.abs(x), x < 0, np.zeros(X.shape, dtype=np.int64)
+    return None
+
+
 def _matmul(a, b):
     """enc[B] @ X[B, D] (logistic_regression/trainer.py:166): per output j,
     Prod_i base_i^(k'_ij * 2^(d_ij)) with base_i = c_i or c_i^-1 (negative
@@ -211,20 +238,28 @@ def _matmul(a, b):
     _check_same_key(list(A))
     ctx = A[0].context
     Bn, D = X.shape
-    thr = ctx.min_value_for_negative
-    ks = [[0] * D for _ in range(Bn)]
-    neg = [[False] * D for _ in range(Bn)]
-    ex = np.zeros((Bn, D), dtype=np.int64)
-    for i in range(Bn):
-        for j in range(D):
-            s = X[i, j].item()
-            e = PaillierEncoder.cal_exponent(s, precision=None)
-            k = int(PaillierEncoder.encode_single(ctx, s, e))
-            if k >= thr:
-                ks[i][j], neg[i][j] = ctx.n - k, True
-            else:
-                ks[i][j] = k
-            ex[i, j] = A[i].exponent + e
+    cexp = np.array([c.exponent for c in A], dtype=np.int64)
+    vec = _encode_scalars_vec(X)
+    if vec is not None:
+        kabs, neg_a, e_a = vec
+        ks = kabs.tolist()
+        neg = neg_a.tolist()
+        ex = cexp[:, None] + e_a
+    else:
+        thr = ctx.min_value_for_negative
+        ks = [[0] * D for _ in range(Bn)]
+        neg = [[False] * D for _ in range(Bn)]
+        ex = np.zeros((Bn, D), dtype=np.int64)
+        for i in range(Bn):
+            for j in range(D):
+                s = X[i, j].item()
+                e = PaillierEncoder.cal_exponent(s, precision=None)
+                k = int(PaillierEncoder.encode_single(ctx, s, e))
+                if k >= thr:
+                    ks[i][j], neg[i][j] = ctx.n - k, True
+                else:
+                    ks[i][j] = k
+                ex[i, j] = cexp[i] + e
     emin = ex.min(axis=0)
     need_inv = [i for i in range(Bn) if any(neg[i])]
     # bases: the B ciphertexts, then the inverses of those with a negative scalar
