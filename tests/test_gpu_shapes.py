@@ -109,12 +109,13 @@ def test_djn_encrypt_both_shapes():
         for win in (16, 7):
             dk = DeviceKey(g["key_bits"], n, p, q, h, win_bits=win)
             rng = random.Random(win)
-            ms = [rng.randrange(n) for _ in range(BIG)]
-            rs = [rng.randrange(1, 1 << dk.rand_bits) for _ in range(BIG)]
+            nbig = 24000  # above the 16-lane encryption limit (20,480)
+            ms = [rng.randrange(n) for _ in range(nbig)]
+            rs = [rng.randrange(1, 1 << dk.rand_bits) for _ in range(nbig)]
             mw, rw = ints_to_words(ms, dk.nw), ints_to_words(rs, dk.rand_words)
             big = words_to_ints(dk.encrypt_words(mw, rw))
             small = words_to_ints(dk.encrypt_words(mw[:SMALL], rw[:SMALL]))
             assert small == big[:SMALL]
             ok = O.derive_private(p, q, h)
-            for i in (0, SMALL - 1, BIG - 1):
+            for i in (0, SMALL - 1, nbig - 1):
                 assert big[i] == O.encrypt_m(ok, ms[i], rs[i])

@@ -194,7 +194,7 @@ inline BigU modinv(const BigU& a, const BigU& m) {
 // words, O(bits^2 / 64) word operations: ~1 ms at 4096 bits); returns false
 // when gcd(x, m) != 1. Used for the one inverse per batch at the root of the
 // device product tree (batch inversion, utils.py:71-76 semantics).
-inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uint32_t* out32) {
+inline bool modinv_words_binary(const uint32_t* x32, const uint32_t* m32, int nw32, uint32_t* out32) {
   const int W = (nw32 + 1) / 2 + 1;  // one spare word for (a + m) before halving
   std::vector<uint64_t> u(W, 0), v(W, 0), x1(W, 0), x2(W, 0), m(W, 0);
   for (int i = 0; i < nw32; ++i) {
@@ -268,6 +268,174 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
   const std::vector<uint64_t>& r = is_one(u) ? x1 : x2;
   for (int i = 0; i < nw32; ++i) out32[i] = (uint32_t)(r[i / 2] >> (32 * (i & 1)));
   return true;
+}
+
+// x^-1 mod m for odd m, x < m: the binary extended GCD with the iterations
+// batched 31 at a time (the approach of T. Pornin, "Optimized Binary GCD for
+// Modular Inversion", 2020). A batch runs on 64-bit approximations of a and b
+// (their low 31 bits, exact, and their top 33 bits at a common position): the
+// parity tests are exact, the comparisons approximate; the batch's 2x2 update
+// matrix (entries <= 2^31) is then applied once to the full-width a, b and to
+// the Bezout cofactors u, v mod m (each divided by 2^31 with one Montgomery
+// step), and a row that came out negative is negated. About 2 len(m) / 31
+// batches of a few linear passes, instead of ~2 len(m) full-width shift /
+// subtract passes. Returns false when gcd(x, m) != 1; falls back to the plain
+// binary algorithm if the batch budget runs out (never observed).
+inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uint32_t* out32) {
+  if (nw32 <= 0 || !(m32[0] & 1)) return modinv_words_binary(x32, m32, nw32, out32);
+  const int W = (nw32 + 1) / 2 + 1;
+  using u64 = uint64_t;
+  using i128 = __int128;
+  std::vector<u64> a(W, 0), b(W, 0), u(W, 0), v(W, 0), m(W, 0), t(W + 1, 0);
+  for (int i = 0; i < nw32; ++i) {
+    a[i / 2] |= (u64)x32[i] << (32 * (i & 1));
+    m[i / 2] |= (u64)m32[i] << (32 * (i & 1));
+  }
+  b = m;
+  u[0] = 1;
+  auto bitlen = [&](const std::vector<u64>& x) {
+    for (int i = W - 1; i >= 0; --i)
+      if (x[i]) return 64 * i + 64 - __builtin_clzll(x[i]);
+    return 0;
+  };
+  auto is_zero = [&](const std::vector<u64>& x) {
+    for (int i = 0; i < W; ++i)
+      if (x[i]) return false;
+    return true;
+  };
+  auto geq = [&](const std::vector<u64>& x, const std::vector<u64>& y) {
+    for (int i = W - 1; i >= 0; --i)
+      if (x[i] != y[i]) return x[i] > y[i];
+    return true;
+  };
+  if (!geq(m, a) || (geq(a, m) && geq(m, a))) return modinv_words_binary(x32, m32, nw32, out32);  // x >= m
+  auto bits_at = [&](const std::vector<u64>& x, int pos) -> u64 {  // 64 bits of x from bit pos
+    int w = pos >> 6, sh = pos & 63;
+    u64 lo = w < W ? x[w] : 0, hi = w + 1 < W ? x[w + 1] : 0;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  };
+  // r = (f x + g y) / 2^31, exact; returns true when negative (r then holds
+  // the magnitude)
+  auto lin_shift = [&](int64_t f, const std::vector<u64>& x, int64_t g, const std::vector<u64>& y,
+                       std::vector<u64>& r) {
+    i128 c = 0;
+    for (int i = 0; i < W; ++i) {
+      c += (i128)f * (i128)x[i] + (i128)g * (i128)y[i];
+      t[i] = (u64)c;
+      c >>= 64;
+    }
+    t[W] = (u64)(int64_t)c;
+    bool neg = (int64_t)t[W] < 0;
+    if (neg) {  // two's complement negate over W+1 words
+      unsigned carry = 1;
+      for (int i = 0; i <= W; ++i) {
+        u64 nv = ~t[i] + carry;
+        carry = (carry && nv == 0) ? 1 : 0;
+        t[i] = nv;
+      }
+    }
+    for (int i = 0; i < W; ++i) r[i] = (t[i] >> 31) | (t[i + 1] << 33);
+    return neg;
+  };
+  // -m^-1 mod 2^64 (Newton)
+  u64 minv = 1;
+  for (int i = 0; i < 6; ++i) minv *= 2 - m[0] * minv;
+  const u64 mneg_inv = (u64)0 - minv;
+  const u64 M31 = (1ull << 31) - 1;
+  // r = (f x + g y) 2^-31 mod m, x, y in [0, m)
+  auto lin_mod = [&](int64_t f, const std::vector<u64>& x, int64_t g, const std::vector<u64>& y,
+                     std::vector<u64>& r) {
+    i128 c = 0;
+    for (int i = 0; i < W; ++i) {
+      c += (i128)f * (i128)x[i] + (i128)g * (i128)y[i];
+      t[i] = (u64)c;
+      c >>= 64;
+    }
+    t[W] = (u64)(int64_t)c;
+    const u64 q = (t[0] * mneg_inv) & M31;  // t + q m = 0 (mod 2^31)
+    unsigned __int128 cc = 0;
+    i128 sc = 0;
+    for (int i = 0; i < W; ++i) {
+      cc += (unsigned __int128)t[i] + (unsigned __int128)q * m[i];
+      t[i] = (u64)cc;
+      cc >>= 64;
+    }
+    sc = (i128)(int64_t)t[W] + (i128)(u64)cc;
+    t[W] = (u64)sc;
+    // shift right 31 (arithmetic), value in (-3m, 3m)
+    for (int i = 0; i < W; ++i) r[i] = (t[i] >> 31) | (t[i + 1] << 33);
+    int64_t top = (int64_t)t[W] >> 31;  // sign word of the shifted value (0 or -1)
+    // bring into [0, m)
+    for (int it = 0; it < 4 && top < 0; ++it) {  // add m
+      unsigned __int128 k2 = 0;
+      for (int i = 0; i < W; ++i) {
+        k2 += (unsigned __int128)r[i] + m[i];
+        r[i] = (u64)k2;
+        k2 >>= 64;
+      }
+      top += (int64_t)k2;
+    }
+    while (geq(r, m)) {
+      u64 br = 0;
+      for (int i = 0; i < W; ++i) {
+        unsigned __int128 d = (unsigned __int128)r[i] - m[i] - br;
+        r[i] = (u64)d;
+        br = (u64)(d >> 64) & 1;
+      }
+    }
+  };
+  std::vector<u64> na(W), nb(W), nu(W), nv(W);
+  const int max_batches = (2 * 64 * W) / 31 + 16;
+  for (int batch = 0; batch < max_batches; ++batch) {
+    if (is_zero(a)) {
+      // b = gcd(x, m)
+      if (b[0] != 1) return false;
+      for (int i = 1; i < W; ++i)
+        if (b[i]) return false;
+      for (int i = 0; i < nw32; ++i) out32[i] = (uint32_t)(v[i / 2] >> (32 * (i & 1)));
+      return true;
+    }
+    const int n = std::max(std::max(bitlen(a), bitlen(b)), 64);
+    u64 xa, xb;
+    if (n <= 64) {
+      xa = a[0];
+      xb = b[0];
+    } else {
+      xa = (bits_at(a, n - 33) << 31) | (a[0] & M31);
+      xb = (bits_at(b, n - 33) << 31) | (b[0] & M31);
+    }
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    for (int j = 0; j < 31; ++j) {
+      if (xa & 1) {
+        if (xa < xb) {
+          std::swap(xa, xb);
+          std::swap(f0, f1);
+          std::swap(g0, g1);
+        }
+        xa -= xb;
+        f0 -= f1;
+        g0 -= g1;
+      }
+      xa >>= 1;
+      f1 <<= 1;
+      g1 <<= 1;
+    }
+    if (lin_shift(f0, a, g0, b, na)) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (lin_shift(f1, a, g1, b, nb)) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    lin_mod(f0, u, g0, v, nu);
+    lin_mod(f1, u, g1, v, nv);
+    a.swap(na);
+    b.swap(nb);
+    u.swap(nu);
+    v.swap(nv);
+  }
+  return modinv_words_binary(x32, m32, nw32, out32);
 }
 
 // a^e mod m, plain square-and-multiply (key setup only)
