@@ -39,6 +39,9 @@ namespace xhe {
 #ifndef XHE_SQ_LDS
 #define XHE_SQ_LDS 1  // variable-base exponentiations: squaring operand through LDS (SqLds)
 #endif
+#ifndef XHE_DJN_FOLD
+#define XHE_DJN_FOLD 1  // k_djn_pow_lds: (1 + n m) as the last (plain) multiplier, nwin + 1 products
+#endif
 #ifndef XHE_M_MAD
 #define XHE_M_MAD 0  // Montgomery digit m = x0 * n0inv by v_mad_u64_u32 instead of v_mul_lo_u32
 #endif

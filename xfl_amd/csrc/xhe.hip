@@ -209,6 +209,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   struct {
     ModOff p2, q2, p, q, p2L, q2L, p2X, q2X;
     size_t nR2C_p2X = 0, nR2C_q2X = 0, R1C_p2X = 0, R1C_q2X = 0;
+    size_t nR_p2 = 0, nR_q2 = 0;
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
@@ -230,6 +231,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     // n R^2 mod P^2
     o.nR2_p2 = bl.put_limbs(mulmod(mod(n, p2), mulmod(Rp2, Rp2, p2), p2), s2);
     o.nR2_q2 = bl.put_limbs(mulmod(mod(n, q2), mulmod(Rq2, Rq2, q2), q2), s2);
+    o.nR_p2 = bl.put_limbs(mulmod(mod(n, p2), Rp2, p2), s2);  // n R mod P^2
+    o.nR_q2 = bl.put_limbs(mulmod(mod(n, q2), Rq2, q2), s2);
     // CRT constants (context.py:46)
     BigU q2inv = modinv(q2, p2);
     o.q2invR = bl.put_limbs(mulmod(q2inv, Rp2, p2), s2);
@@ -313,6 +316,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.q2X = moddev(B, o.q2X);
     kd.q2 = moddev(B, o.q2);
     kd.nR2_p2 = B + o.nR2_p2;
+    kd.nR_p2 = B + o.nR_p2;
+    kd.nR_q2 = B + o.nR_q2;
     kd.nR2C_p2X = B + o.nR2C_p2X;
     kd.nR2C_q2X = B + o.nR2C_q2X;
     kd.R1C_p2X = B + o.R1C_p2X;

@@ -43,6 +43,7 @@ struct KeyDev {
   ModDev p2X, q2X;            // and in the 16-lane (one DPP row) decrypt shape
   ModDev n2X;                 // n^2 in the 16-lane shape (small-batch ciphertext ops)
   const uint32_t* nR2_p2;     // n * R^2 mod p^2
+  const uint32_t *nR_p2, *nR_q2;  // n * R mod P^2 (plain n m from a Montgomery product)
   // 16-lane (p2X/q2X, R' = 2^(W*80)) DJN shape on the one-lane tables: every
   // table product scales by R/R', so the start value carries C = (R'/R)^nwin:
   const uint32_t *nR2C_p2X, *nR2C_q2X;  // n * C * R'^2 mod P^2
@@ -272,6 +273,42 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
 
+// The squaring operand of an exponentiation, parked in LDS instead of a
+// global workspace row (a squaring reads back the 74-152 limbs it just
+// wrote: through LDS that round trip never leaves the CU). Per wave: 64 / TPI
+// residues of S4 words. TPI == 1: quad-major image [quad][lane][4 words]
+// (ds_write_b128 / ds_read_b128, conflict-free); TPI > 1: one contiguous row
+// per lane group, read by the whole group (broadcast).
+template <class M_>
+struct SqLds {
+  static constexpr int WORDS_PER_WAVE = 64 / M_::TPI * M_::S4;
+  uint32_t* slot;
+  XHE_DEV explicit SqLds(uint32_t* wave_img) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (M_::TPI == 1) slot = wave_img + lane * 4;
+    else slot = wave_img + (lane / M_::TPI) * M_::S4;
+  }
+  XHE_DEV void put(const uint32_t (&b)[M_::L]) const {
+    if constexpr (M_::TPI == 1) {
+#pragma unroll
+      for (int q = 0; q < M_::S4 / 4; ++q) {
+        uint4 v = make_uint4(4 * q < M_::S ? b[4 * q] : 0u, 4 * q + 1 < M_::S ? b[4 * q + 1] : 0u,
+                             4 * q + 2 < M_::S ? b[4 * q + 2] : 0u, 4 * q + 3 < M_::S ? b[4 * q + 3] : 0u);
+        *reinterpret_cast<uint4*>(slot + q * 256) = v;
+      }
+    } else {
+      const int g = M_::G::g();
+#pragma unroll
+      for (int j = 0; j < M_::L; ++j) slot[g * M_::L + j] = b[j];
+    }
+    wave_sync_mem_();
+  }
+  XHE_DEV uint4 load4(int i) const {
+    if constexpr (M_::TPI == 1) return *reinterpret_cast<const uint4*>(slot + (i >> 2) * 256);
+    else return *reinterpret_cast<const uint4*>(slot + i);
+  }
+};
+
 // A table row of RS4 words read by a wider-shape Montgomery product (limbs
 // beyond the row are zero).
 template <int RS4>
@@ -330,30 +367,62 @@ struct ALdsQ {
 
 // c_P = (1 + n m) h^a mod P^2 for one element and one prime, table rows
 // through the wave's LDS image; written as row `prime` of ws.
+// XHE_DJN_FOLD: the product starts from the first window's row (h_0 R) and
+// (1 + n m) enters once, in plain form, as the last multiplier, so the
+// conversion out of Montgomery form is that same product: nwin + 1 products
+// instead of nwin + 2 ((1 + n m) R first, a final multiply by 1).
 template <class MP2>
 XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, const ModDev& md,
-                           const uint32_t* tab, const uint32_t* nR2, const uint32_t* __restrict__ m_words,
-                           const uint32_t* __restrict__ a_words, int aw, int64_t count, int64_t e, int prime,
-                           uint32_t* img, const uint32_t* mine, uint32_t* __restrict__ ws) {
+                           const uint32_t* tab, const uint32_t* nR2, const uint32_t* nR,
+                           const uint32_t* __restrict__ m_words, const uint32_t* __restrict__ a_words, int aw,
+                           int64_t count, int64_t e, int prime, uint32_t* img, const uint32_t* mine,
+                           uint32_t* __restrict__ ws) {
   constexpr int NQ = MP2::S4 / 4;
   MP2 M;
   M.init(Np, md.n0inv);
   uint32_t b[MP2::L];
-  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
-  M.mul(b, ARow{nR2});     // n m R mod P^2
-  M.add_row(b, md.R1);     // (1 + n m) R
   const uint32_t* ae = a_words + (size_t)e * aw;
   const int rows = 1 << key.win;
-  for (int w = 0; w < key.nwin; ++w) {
+  auto stage = [&](int w) {
     uint32_t d = digit_at(ae, aw, w * key.win, key.win);
     const uint32_t* row = tab + ((size_t)w * rows + d) * MP2::S4;
 #pragma unroll
     for (int k = 0; k < NQ; ++k)
       __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+#if XHE_DJN_FOLD
+  (void)nR2;
+  stage(0);
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const uint4 v = ALdsQ{mine}.load4(4 * k);
+    if (4 * k < MP2::S) b[4 * k] = v.x;
+    if (4 * k + 1 < MP2::S) b[4 * k + 1] = v.y;
+    if (4 * k + 2 < MP2::S) b[4 * k + 2] = v.z;
+    if (4 * k + 3 < MP2::S) b[4 * k + 3] = v.w;
+  }
+  for (int w = 1; w < key.nwin; ++w) {
+    stage(w);
+    M.mul(b, ALdsQ{mine});
+  }
+  // park h^a R in this lane's slot of the image (quad-major, as a staged row)
+  SqLds<MP2>(img).put(b);
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{nR});  // n m mod P^2 (< 2 P^2), plain
+  b[0] += 1u;          // 1 + n m: one limb may reach 2^W, inside the lazy-carry bound
+  M.mul(b, ALdsQ{mine});  // (1 + n m) h^a mod P^2
+#else
+  (void)nR;
+  M.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  M.mul(b, ARow{nR2});     // n m R mod P^2
+  M.add_row(b, md.R1);     // (1 + n m) R
+  for (int w = 0; w < key.nwin; ++w) {
+    stage(w);
     M.mul(b, ALdsQ{mine});
   }
   M.mul(b, AOne{});
+#endif
   M.reduce_once(b);
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
@@ -371,8 +440,8 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
   const int prime = blockIdx.y;
   uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
   djn_prime_lds<MP2>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
-                     prime ? key.nR2_q2 : key.nR2_p2, m_words, a_words, aw, count, e, prime, img,
-                     img + (threadIdx.x & 63) * 4, ws);
+                     prime ? key.nR2_q2 : key.nR2_p2, prime ? key.nR_q2 : key.nR_p2, m_words, a_words, aw, count, e,
+                     prime, img, img + (threadIdx.x & 63) * 4, ws);
 }
 
 #endif
@@ -429,42 +498,6 @@ __global__ void __launch_bounds__(256, 2) k_raw_enc(KeyDev key, const uint32_t* 
 // k_dec_pow: X_P = (c^(P-1) mod P^2) - 1 for one prime (grid.y), written to
 // xrows [prime][S4][count]. Per-group 4-bit window tables live in wsg
 // (17 interleaved rows per group, grid-stride loop over elements).
-// The squaring operand of an exponentiation, parked in LDS instead of a
-// global workspace row (a squaring reads back the 74-152 limbs it just
-// wrote: through LDS that round trip never leaves the CU). Per wave: 64 / TPI
-// residues of S4 words. TPI == 1: quad-major image [quad][lane][4 words]
-// (ds_write_b128 / ds_read_b128, conflict-free); TPI > 1: one contiguous row
-// per lane group, read by the whole group (broadcast).
-template <class M_>
-struct SqLds {
-  static constexpr int WORDS_PER_WAVE = 64 / M_::TPI * M_::S4;
-  uint32_t* slot;
-  XHE_DEV explicit SqLds(uint32_t* wave_img) {
-    const int lane = threadIdx.x & 63;
-    if constexpr (M_::TPI == 1) slot = wave_img + lane * 4;
-    else slot = wave_img + (lane / M_::TPI) * M_::S4;
-  }
-  XHE_DEV void put(const uint32_t (&b)[M_::L]) const {
-    if constexpr (M_::TPI == 1) {
-#pragma unroll
-      for (int q = 0; q < M_::S4 / 4; ++q) {
-        uint4 v = make_uint4(4 * q < M_::S ? b[4 * q] : 0u, 4 * q + 1 < M_::S ? b[4 * q + 1] : 0u,
-                             4 * q + 2 < M_::S ? b[4 * q + 2] : 0u, 4 * q + 3 < M_::S ? b[4 * q + 3] : 0u);
-        *reinterpret_cast<uint4*>(slot + q * 256) = v;
-      }
-    } else {
-      const int g = M_::G::g();
-#pragma unroll
-      for (int j = 0; j < M_::L; ++j) slot[g * M_::L + j] = b[j];
-    }
-    wave_sync_mem_();
-  }
-  XHE_DEV uint4 load4(int i) const {
-    if constexpr (M_::TPI == 1) return *reinterpret_cast<const uint4*>(slot + (i >> 2) * 256);
-    else return *reinterpret_cast<const uint4*>(slot + i);
-  }
-};
-
 template <class MP2>
 XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* ex, int ebits,
                              uint32_t* tab, uint32_t* sq, int st, uint32_t* sq_lds = nullptr) {
