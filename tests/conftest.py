@@ -20,7 +20,7 @@ try:
         _torch.cuda.init()
 except Exception:  # no torch / no GPU: CPU-only runs
     pass
-FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json"]
+FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json", "paillier_4096_djn.json"]
 
 
 def pytest_configure(config):

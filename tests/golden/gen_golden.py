@@ -270,7 +270,8 @@ def main():
     warnings.simplefilter("ignore")
     specs = [("paillier_2048_djn.json", 2048, True, 11, 48),
              ("paillier_2048_nodjn.json", 2048, False, 12, 24),
-             ("paillier_3072_djn.json", 3072, True, 13, 16)]
+             ("paillier_3072_djn.json", 3072, True, 13, 16),
+             ("paillier_4096_djn.json", 4096, True, 14, 16)]
     only = set(sys.argv[1:])
     for fname, bits, djn, seed, nvec in specs:
         if only and fname not in only:

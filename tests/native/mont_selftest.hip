@@ -103,6 +103,8 @@ int main() {
     rc |= run<Mont<56, 28, 2>>(1536, rng, mode);
     rc |= run<Mont<152, 27, 4>>(4096, rng, mode);
     rc |= run<Mont<76, 27, 4>>(2048, rng, mode);
+    rc |= run<Mont<160, 27, 16>>(4096, rng, mode);
+    rc |= run<Mont<304, 27, 16>>(8192, rng, mode);
   }
   return rc;
 }

@@ -34,7 +34,7 @@ def _raw(arr):
 
 
 @pytest.mark.parametrize("vectorized", [False, True])
-@pytest.mark.parametrize("fx", FIXTURES[:2])
+@pytest.mark.parametrize("fx", FIXTURES)
 def test_ops_bit_exact(fx, vectorized):
     """vectorized=False: numpy's per-element object loop over PaillierCiphertext
     operators; True: PaillierArray's batched kernels (segmented product,
@@ -234,3 +234,27 @@ def test_deferred_sums_groupby_and_chains():
     assert (s2.raw_ciphertext, s2.exponent) == want
     m = s2 * 3
     assert m.raw_ciphertext == O.mul_ct(ok, want[0], want[1], 3)[0]
+
+
+@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+def test_larger_keys_tolerance_ops(fx):
+    """The reference's tolerance checks (test_paillier.py:24-296) on the
+    3072/4096-bit fixture keys (the operators offer key_bit_size 4096,
+    config_descriptor/vertical_logistic_regression/label_trainer.py:118):
+    private and public encryption, +, -, scalar *, / and the batch sum, in
+    batches large enough to take the one-lane-per-residue kernels."""
+    from xfl_amd.paillier import Paillier
+    priv, pub = _ctxs(load_fixture(fx))
+    rng = np.random.default_rng(5)
+    p1 = (rng.random(30000) * 100 - 50).astype(np.float32)
+    p2 = (rng.random(30000) * 100 - 20).astype(np.float32)
+    c1 = Paillier.encrypt(priv, p1, precision=7)
+    c2 = Paillier.encrypt(pub, p2, precision=7)
+    assert np.all(np.abs(Paillier.decrypt(priv, c1) - p1) < 1e-4)
+    assert np.all(np.abs(Paillier.decrypt(priv, c2) - p2) < 1e-4)
+    s1, s2, c1s, c2s = p1[:64], p2[:64], c1[:64], c2[:64]
+    assert np.all(np.abs(Paillier.decrypt(priv, c1s + c2s) - (s1 + s2)) < 1e-4)
+    assert np.all(np.abs(Paillier.decrypt(priv, c1s - c2s) - (s1 - s2)) < 1e-4)
+    assert np.all(np.abs(Paillier.decrypt(priv, c1s * s2) - (s1 * s2)) < 1e-2)
+    assert np.all(np.abs(Paillier.decrypt(priv, c1s / s2) - (s1 / s2)) < 1e-4)
+    assert abs(Paillier.decrypt(priv, sum(c1s)) - np.sum(s1.astype(np.float64))) < 1e-2

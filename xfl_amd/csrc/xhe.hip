@@ -55,6 +55,30 @@ struct Shape3072 {
   using MN2 = Mont<228, 27, 4>;
   using MN2X = Mont<240, 27, 16>;
 };
+// 4096-bit keys (the LR/LinReg/Pearson/WoE operators' OneOf(2048, 4096, 8192)):
+// 28-bit limbs would overflow the lazy 64-bit accumulator at S = 147
+// ((2S+2) 2^56 >= 2^64), so every modulus uses 27-bit limbs. p^2 residues
+// take 4 lanes (38 limbs each), n^2 residues one 16-lane DPP row (19 each)
+// in both the batch and the small-batch shapes; the mod-p limbs share W with
+// p^2 so k_dec_fin reads k_dec_pow's rows unchanged.
+struct Shape4096 {
+  using MP2 = Mont<152, 27, 4>;
+  using MP2L = Mont<152, 27, 4>;
+  using MP2X = Mont<160, 27, 16>;
+  using MP = Mont<76, 27, 4>;
+  using MN2 = Mont<304, 27, 16>;
+  using MN2X = Mont<304, 27, 16>;
+};
+
+constexpr bool key_bits_supported(int K) { return K == 2048 || K == 3072 || K == 4096; }
+
+// Calls f(ShapeK{}) for the key size K (checked at xhe_key_create).
+template <class F>
+decltype(auto) with_shape(int K, F&& f) {
+  if (K == 2048) return f(Shape2048{});
+  if (K == 3072) return f(Shape3072{});
+  return f(Shape4096{});
+}
 
 struct ModSpec {
   int S, W;
@@ -355,8 +379,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       const ModDev mds[2] = {kd.p2, kd.q2};
       const uint32_t* hms[2] = {B + o.hM_p2, B + o.hM_q2};
       uint32_t* tabs[2] = {k->d_tab, k->d_tab + tab_words};
-      if (K == 2048) build_tables_sync<Shape2048::MP2>(k, mds, hms, tabs, 2);
-      else build_tables_sync<Shape3072::MP2>(k, mds, hms, tabs, 2);
+      with_shape(K, [&](auto sh) { build_tables_sync<typename decltype(sh)::MP2>(k, mds, hms, tabs, 2); });
     }
   }
   if (!k->priv && k->djn) {
@@ -368,8 +391,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.tab_n2 = k->d_tab;
     const uint32_t* hm = B + o_hMn2;
     uint32_t* tab = k->d_tab;
-    if (K == 2048) build_tables_sync<Shape2048::MN2>(k, &kd.n2, &hm, &tab, 1);
-    else build_tables_sync<Shape3072::MN2>(k, &kd.n2, &hm, &tab, 1);
+    with_shape(K, [&](auto sh) { build_tables_sync<typename decltype(sh)::MN2>(k, &kd.n2, &hm, &tab, 1); });
   }
 }
 
@@ -879,13 +901,11 @@ int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev,
     DevGuard dg(key->device);
     const bool row = n2_row(count);
     hipStream_t hs = (hipStream_t)stream;
-    if (key->K == 2048) {
-      if (row) segprod_impl<Shape2048, Shape2048::MN2X>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
-      else segprod_impl<Shape2048>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
-    } else {
-      if (row) segprod_impl<Shape3072, Shape3072::MN2X>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
-      else segprod_impl<Shape3072>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
-    }
+    with_shape(key->K, [&](auto sh) {
+      using Sh = decltype(sh);
+      if (row) segprod_impl<Sh, typename Sh::MN2X>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+      else segprod_impl<Sh>(key, c_dev, d_dev, dmax, count, seg_begin, nseg, out_dev, hs);
+    });
     return XHE_OK;
   });
 }
@@ -930,8 +950,8 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
   return guarded([&]() -> int {
     if (!out || !n_words) return fail(XHE_EINVAL, "xhe_key_create: null argument");
     *out = nullptr;
-    if (key_bits != 2048 && key_bits != 3072)
-      return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048 or 3072");
+    if (!key_bits_supported(key_bits))
+      return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048, 3072 or 4096");
     if ((p_words == nullptr) != (q_words == nullptr)) return fail(XHE_EINVAL, "xhe_key_create: need both p and q");
     if (win_bits == 0) {
       const char* ev = getenv("XHE_WIN_BITS");
@@ -946,21 +966,15 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     k->n2w = 2 * k->nw;
     k->priv = p_words != nullptr;
     k->djn = h_pow_n_words != nullptr;
-    if (key_bits == 2048) {
-      k->mp2 = {Shape2048::MP2::S, Shape2048::MP2::W};
-      k->mp2L = {Shape2048::MP2L::S, Shape2048::MP2L::W};
-      k->mp2X = {Shape2048::MP2X::S, Shape2048::MP2X::W};
-      k->mp = {Shape2048::MP::S, Shape2048::MP::W};
-      k->mn2 = {Shape2048::MN2::S, Shape2048::MN2::W};
-      k->mn2X = {Shape2048::MN2X::S, Shape2048::MN2X::W};
-    } else {
-      k->mp2 = {Shape3072::MP2::S, Shape3072::MP2::W};
-      k->mp2L = {Shape3072::MP2L::S, Shape3072::MP2L::W};
-      k->mp2X = {Shape3072::MP2X::S, Shape3072::MP2X::W};
-      k->mp = {Shape3072::MP::S, Shape3072::MP::W};
-      k->mn2 = {Shape3072::MN2::S, Shape3072::MN2::W};
-      k->mn2X = {Shape3072::MN2X::S, Shape3072::MN2X::W};
-    }
+    with_shape(key_bits, [&](auto sh) {
+      using Sh = decltype(sh);
+      k->mp2 = {Sh::MP2::S, Sh::MP2::W};
+      k->mp2L = {Sh::MP2L::S, Sh::MP2L::W};
+      k->mp2X = {Sh::MP2X::S, Sh::MP2X::W};
+      k->mp = {Sh::MP::S, Sh::MP::W};
+      k->mn2 = {Sh::MN2::S, Sh::MN2::W};
+      k->mn2X = {Sh::MN2X::S, Sh::MN2X::W};
+    });
     BigU n = BigU::from_words(n_words, k->nw);
     if ((int)n.bits() > key_bits || n.bits() + 2 < (size_t)key_bits)
       return fail(XHE_EINVAL, "xhe_key_create: n does not match key_bits");
@@ -1042,19 +1056,15 @@ int xhe_encrypt(const xhe_key* key, const uint32_t* m_dev, const uint32_t* rand_
     DevGuard dg(key->device);
     hipStream_t s = (hipStream_t)stream;
     if (!rand_dev) {
-      if (key->K == 2048) raw_encrypt_impl<Shape2048>(key, m_dev, count, ct_dev, s);
-      else raw_encrypt_impl<Shape3072>(key, m_dev, count, ct_dev, s);
+      with_shape(key->K, [&](auto sh) { raw_encrypt_impl<decltype(sh)>(key, m_dev, count, ct_dev, s); });
       return XHE_OK;
     }
     if (key->djn && key->priv) {
-      if (key->K == 2048) encrypt_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
-      else encrypt_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+      with_shape(key->K, [&](auto sh) { encrypt_impl<decltype(sh)>(key, m_dev, rand_dev, count, ct_dev, s); });
     } else if (key->djn) {
-      if (key->K == 2048) encrypt_pub_djn_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
-      else encrypt_pub_djn_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+      with_shape(key->K, [&](auto sh) { encrypt_pub_djn_impl<decltype(sh)>(key, m_dev, rand_dev, count, ct_dev, s); });
     } else {
-      if (key->K == 2048) encrypt_nodjn_impl<Shape2048>(key, m_dev, rand_dev, count, ct_dev, s);
-      else encrypt_nodjn_impl<Shape3072>(key, m_dev, rand_dev, count, ct_dev, s);
+      with_shape(key->K, [&](auto sh) { encrypt_nodjn_impl<decltype(sh)>(key, m_dev, rand_dev, count, ct_dev, s); });
     }
     return XHE_OK;
   });
@@ -1066,8 +1076,7 @@ int xhe_decrypt(const xhe_key* key, const uint32_t* ct_dev, int64_t count, uint3
     if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    if (key->K == 2048) decrypt_impl<Shape2048>(key, ct_dev, count, m_dev, (hipStream_t)stream);
-    else decrypt_impl<Shape3072>(key, ct_dev, count, m_dev, (hipStream_t)stream);
+    with_shape(key->K, [&](auto sh) { decrypt_impl<decltype(sh)>(key, ct_dev, count, m_dev, (hipStream_t)stream); });
     return XHE_OK;
   });
 }
@@ -1138,13 +1147,11 @@ int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev,
     DevGuard dg(key->device);
     const bool row = n2_row(count);
     hipStream_t hs = (hipStream_t)stream;
-    if (key->K == 2048) {
-      if (row) mulmod_impl<Shape2048, Shape2048::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
-      else mulmod_impl<Shape2048>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
-    } else {
-      if (row) mulmod_impl<Shape3072, Shape3072::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
-      else mulmod_impl<Shape3072>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
-    }
+    with_shape(key->K, [&](auto sh) {
+      using Sh = decltype(sh);
+      if (row) mulmod_impl<Sh, typename Sh::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+      else mulmod_impl<Sh>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+    });
     return XHE_OK;
   });
 }
@@ -1158,13 +1165,11 @@ int xhe_powmod(const xhe_key* key, const uint32_t* c_dev, const uint32_t* k_dev,
     DevGuard dg(key->device);
     const bool row = n2_row(count);
     hipStream_t hs = (hipStream_t)stream;
-    if (key->K == 2048) {
-      if (row) powmod_impl<Shape2048, Shape2048::MN2X>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
-      else powmod_impl<Shape2048>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
-    } else {
-      if (row) powmod_impl<Shape3072, Shape3072::MN2X>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
-      else powmod_impl<Shape3072>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
-    }
+    with_shape(key->K, [&](auto sh) {
+      using Sh = decltype(sh);
+      if (row) powmod_impl<Sh, typename Sh::MN2X>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+      else powmod_impl<Sh>(key, c_dev, k_dev, kw, kbits, count, out_dev, hs);
+    });
     return XHE_OK;
   });
 }
@@ -1176,11 +1181,11 @@ int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_
     DevGuard dg(key->device);
     const bool row = n2_row(count);
     hipStream_t hs = (hipStream_t)stream;
-    if (key->K == 2048)
-      return row ? invert_impl<Shape2048, Shape2048::MN2X>(key, c_dev, count, out_dev, hs)
-                 : invert_impl<Shape2048>(key, c_dev, count, out_dev, hs);
-    return row ? invert_impl<Shape3072, Shape3072::MN2X>(key, c_dev, count, out_dev, hs)
-               : invert_impl<Shape3072>(key, c_dev, count, out_dev, hs);
+    return with_shape(key->K, [&](auto sh) -> int {
+      using Sh = decltype(sh);
+      return row ? invert_impl<Sh, typename Sh::MN2X>(key, c_dev, count, out_dev, hs)
+                 : invert_impl<Sh>(key, c_dev, count, out_dev, hs);
+    });
   });
 }
 
@@ -1368,24 +1373,21 @@ int xhe_multiexp(const xhe_key* key, const uint32_t* bases_dev, int64_t nbases, 
       return fail(XHE_EINVAL, "xhe_multiexp: problem too large for one call");
     DevGuard dg(key->device);
     const bool row = n2_row(std::max(nbases, ncols));
-    const int s4 = key->K == 2048 ? (row ? Shape2048::MN2X::S4 : Shape2048::MN2::S4)
-                                  : (row ? Shape3072::MN2X::S4 : Shape3072::MN2::S4);
+    const int s4 = with_shape(key->K, [&](auto sh) -> int {
+      using Sh = decltype(sh);
+      return row ? Sh::MN2X::S4 : Sh::MN2::S4;
+    });
     const int c = win_bits ? win_bits : mexp_window(nbases, ncols, nterms, std::max(kbits, 1), s4);
     const int kb = std::max(kbits, 1);
     hipStream_t hs = (hipStream_t)stream;
-    if (key->K == 2048) {
+    with_shape(key->K, [&](auto sh) {
+      using Sh = decltype(sh);
       if (row)
-        multiexp_impl<Shape2048, Shape2048::MN2X>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c,
-                                                  out_dev, hs);
+        multiexp_impl<Sh, typename Sh::MN2X>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev,
+                                             hs);
       else
-        multiexp_impl<Shape2048>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev, hs);
-    } else {
-      if (row)
-        multiexp_impl<Shape3072, Shape3072::MN2X>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c,
-                                                  out_dev, hs);
-      else
-        multiexp_impl<Shape3072>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev, hs);
-    }
+        multiexp_impl<Sh>(key, bases_dev, nbases, idx_dev, k_dev, kw, kb, ncols, nterms, c, out_dev, hs);
+    });
     return XHE_OK;
   });
 }
