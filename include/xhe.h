@@ -37,7 +37,7 @@ typedef struct xhe_key xhe_key;
  * 2^win rows of S4 words per prime: 2048-bit key, win 16: 2 x 1.28 GB;
  * win 20: 2 x 16.6 GB (52 instead of 64 products per prime); win 22:
  * 2 x 59.9 GB (47); win 23: 2 x 114.8 GB (45); 4096-bit key, win 16:
- * 2 x 5.1 GB. key_bits: 2048, 3072 or 4096 (else XHE_ENOTSUP). */
+ * 2 x 5.1 GB. key_bits: 2048, 3072, 4096 or 8192 (else XHE_ENOTSUP). */
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
 void xhe_key_destroy(xhe_key* key);

@@ -20,7 +20,8 @@ try:
         _torch.cuda.init()
 except Exception:  # no torch / no GPU: CPU-only runs
     pass
-FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json", "paillier_4096_djn.json"]
+FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json", "paillier_3072_djn.json", "paillier_4096_djn.json",
+            "paillier_8192_djn.json"]
 
 
 def pytest_configure(config):
@@ -47,6 +48,14 @@ def fl(s):
     return float.fromhex(s)
 
 
+# The pure-Python oracle needs ~3 s per 8192-bit modexp: its CPU checks take
+# the first few vectors of that fixture (the GPU tests check every vector).
+CPU_VECTOR_LIMIT = {"paillier_8192_djn.json": 2}
+
+
 @pytest.fixture(params=FIXTURES)
 def golden(request):
-    return load_fixture(request.param)
+    g = load_fixture(request.param)
+    g["_name"] = request.param
+    g["_cpu_limit"] = CPU_VECTOR_LIMIT.get(request.param)
+    return g

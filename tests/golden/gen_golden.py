@@ -271,7 +271,8 @@ def main():
     specs = [("paillier_2048_djn.json", 2048, True, 11, 48),
              ("paillier_2048_nodjn.json", 2048, False, 12, 24),
              ("paillier_3072_djn.json", 3072, True, 13, 16),
-             ("paillier_4096_djn.json", 4096, True, 14, 16)]
+             ("paillier_4096_djn.json", 4096, True, 14, 16),
+             ("paillier_8192_djn.json", 8192, True, 15, 16)]
     only = set(sys.argv[1:])
     for fname, bits, djn, seed, nvec in specs:
         if only and fname not in only:

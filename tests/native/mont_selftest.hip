@@ -105,6 +105,7 @@ int main() {
     rc |= run<Mont<76, 27, 4>>(2048, rng, mode);
     rc |= run<Mont<160, 27, 16>>(4096, rng, mode);
     rc |= run<Mont<304, 27, 16>>(8192, rng, mode);
+    rc |= run<Mont<640, 26, 16>>(16384, rng, mode);
   }
   return rc;
 }

@@ -236,10 +236,10 @@ def test_deferred_sums_groupby_and_chains():
     assert m.raw_ciphertext == O.mul_ct(ok, want[0], want[1], 3)[0]
 
 
-@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json", "paillier_8192_djn.json"])
 def test_larger_keys_tolerance_ops(fx):
     """The reference's tolerance checks (test_paillier.py:24-296) on the
-    3072/4096-bit fixture keys (the operators offer key_bit_size 4096,
+    3072/4096/8192-bit fixture keys (the operators offer key_bit_size 4096/8192,
     config_descriptor/vertical_logistic_regression/label_trainer.py:118):
     private and public encryption, +, -, scalar *, / and the batch sum, in
     batches large enough to take the one-lane-per-residue kernels."""

@@ -1,0 +1,71 @@
+"""Per-key-size rates on one GPU (2048/3072/4096/8192-bit DJN private keys):
+DJN-CRT encrypt (encode + draw + encrypt, precision 7, obfuscated) and CRT
+decrypt of the same ciphertexts, with the round trip checked bit-exactly.
+
+Keys are the reference-generated fixture keys (tests/golden/paillier_K_djn.json)
+so no host key generation runs here (pure-Python keygen of an 8192-bit DJN
+key takes minutes).
+
+    python tools/bench_keysizes.py [--bits 2048,3072,4096,8192] > profiles/r1/keysizes.jsonl
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from tools.bench_configs import _encrypt_f64, _sync, _timed  # noqa: E402
+
+# elements per timed call: enough lanes to fill the chip in the batch shapes
+N_BY_BITS = {2048: 1_000_000, 3072: 500_000, 4096: 262_144, 8192: 65_536}
+WIN_BY_BITS = {2048: 22, 3072: 20, 4096: 18, 8192: 16}
+
+
+def run(bits, steps):
+    import torch
+    from tests.conftest import hx, load_fixture
+    from xfl_amd import _native as nat
+    L = nat.lib()
+    k = load_fixture(f"paillier_{bits}_djn.json")["key"]
+    p, q, h = hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
+    t0 = time.time()
+    dk = nat.DeviceKey(bits, p * q, p, q, h, device=0, win_bits=WIN_BY_BITS[bits])
+    _sync()
+    tk = time.time() - t0
+    N = N_BY_BITS[bits]
+    x = torch.from_numpy(np.random.default_rng(2).standard_normal(N)).cuda()
+    m = torch.empty((N, dk.nw), dtype=torch.int32, device="cuda")
+    m2 = torch.empty_like(m)
+    ex = torch.empty(N, dtype=torch.int32, device="cuda")
+    st = torch.empty_like(ex)
+    rnd = torch.empty((N, dk.rand_words), dtype=torch.int32, device="cuda")
+    ct = torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    te = _timed(lambda: _encrypt_f64(nat, L, dk, x, 7, m, ex, st, rnd, ct, 1, s), steps)
+    td = _timed(lambda: nat.check(L.xhe_decrypt(dk.handle, ct.data_ptr(), N, m2.data_ptr(), s), "decrypt"), steps)
+    _sync()
+    out = {"key_bits": bits, "elements": N, "fixed_base_window_bits": WIN_BY_BITS[bits],
+           "encrypts_per_s": N / te, "decrypts_per_s": N / td,
+           "roundtrip_bit_exact": bool(torch.equal(m, m2)), "key_setup_s": tk}
+    del dk
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bits", default="2048,3072,4096,8192")
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    for b in [int(v) for v in a.bits.split(",")]:
+        print(json.dumps(run(b, a.steps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

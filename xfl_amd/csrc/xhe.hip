@@ -70,14 +70,27 @@ struct Shape4096 {
   using MN2X = Mont<304, 27, 16>;
 };
 
-constexpr bool key_bits_supported(int K) { return K == 2048 || K == 3072 || K == 4096; }
+// 8192-bit keys: p^2 (8192 bits) in one 16-lane row of 27-bit limbs, p in 4
+// lanes; n^2 (16384 bits) needs 26-bit limbs for the lazy accumulator
+// ((2S+2) 2^52 < 2^64 at S = 640), 40 per lane of a 16-lane row.
+struct Shape8192 {
+  using MP2 = Mont<304, 27, 16>;
+  using MP2L = Mont<304, 27, 16>;
+  using MP2X = Mont<304, 27, 16>;
+  using MP = Mont<152, 27, 4>;
+  using MN2 = Mont<640, 26, 16>;
+  using MN2X = Mont<640, 26, 16>;
+};
+
+constexpr bool key_bits_supported(int K) { return K == 2048 || K == 3072 || K == 4096 || K == 8192; }
 
 // Calls f(ShapeK{}) for the key size K (checked at xhe_key_create).
 template <class F>
 decltype(auto) with_shape(int K, F&& f) {
   if (K == 2048) return f(Shape2048{});
   if (K == 3072) return f(Shape3072{});
-  return f(Shape4096{});
+  if (K == 4096) return f(Shape4096{});
+  return f(Shape8192{});
 }
 
 struct ModSpec {
@@ -951,7 +964,7 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     if (!out || !n_words) return fail(XHE_EINVAL, "xhe_key_create: null argument");
     *out = nullptr;
     if (!key_bits_supported(key_bits))
-      return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048, 3072 or 4096");
+      return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048, 3072, 4096 or 8192");
     if ((p_words == nullptr) != (q_words == nullptr)) return fail(XHE_EINVAL, "xhe_key_create: need both p and q");
     if (win_bits == 0) {
       const char* ev = getenv("XHE_WIN_BITS");

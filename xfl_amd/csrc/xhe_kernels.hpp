@@ -1287,15 +1287,20 @@ __global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __
   int bl = 0;
   // |v| = neg ? n - m : m ; compute words on the fly from the top
   // (borrow needs low words, so compute full magnitude into a small cache)
-  // nw <= 96 for K <= 3072
-  uint32_t mag[96];
-  int64_t br = 0;
-  for (int k = 0; k < nw; ++k) {
-    int64_t d = neg ? ((int64_t)key.n_words[k] - (int64_t)m[k] - br) : (int64_t)m[k];
-    if (neg) { br = d < 0; d += br << 32; }
-    mag[k] = (uint32_t)d;
+  // Word k of |v| without materialising it (nw reaches 256 at 8192 bits):
+  // for v = m - n the borrow into word k is [m mod 2^(32k) > n mod 2^(32k)],
+  // decided by the highest differing word below k (almost always k - 1).
+  auto magw = [&](int k) -> uint32_t {
+    if (!neg) return m[k];
+    uint32_t br = 0;
+    for (int j = k - 1; j >= 0; --j)
+      if (m[j] != key.n_words[j]) { br = m[j] > key.n_words[j]; break; }
+    return key.n_words[k] - m[k] - br;
+  };
+  for (int k = nw - 1; k >= 0; --k) {
+    const uint32_t w = magw(k);
+    if (w) { bl = 32 * k + 32 - __clz(w); break; }
   }
-  for (int k = nw - 1; k >= 0; --k) if (mag[k]) { bl = 32 * k + 32 - __clz(mag[k]); break; }
   double res;
   if (st != 0) { res = 0.0; }
   else if (bl == 0) {
@@ -1306,14 +1311,14 @@ __global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __
     uint64_t mant;
     int shift;
     if (bl <= 53) {
-      mant = (uint64_t)mag[0] | ((uint64_t)(nw > 1 ? mag[1] : 0) << 32);
+      mant = (uint64_t)magw(0) | ((uint64_t)(nw > 1 ? magw(1) : 0) << 32);
       shift = 0;
     } else {
       int s = bl - 53;
       // extract 53 bits starting at bit s, plus round/sticky
       auto bitsat = [&](int pos) -> uint64_t {  // 64 bits starting at pos
         int k = pos >> 5, o = pos & 31;
-        uint64_t w0 = k < nw ? mag[k] : 0, w1 = k + 1 < nw ? mag[k + 1] : 0, w2 = k + 2 < nw ? mag[k + 2] : 0;
+        uint64_t w0 = k < nw ? magw(k) : 0, w1 = k + 1 < nw ? magw(k + 1) : 0, w2 = k + 2 < nw ? magw(k + 2) : 0;
         uint64_t lo = (w0 | (w1 << 32)) >> o;
         if (o) lo |= w2 << (64 - o);
         return lo;
@@ -1321,9 +1326,9 @@ __global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __
       mant = bitsat(s) & ((1ull << 53) - 1);
       uint64_t rbit = (bitsat(s - 1) & 1ull);
       bool sticky = false;
-      for (int k = 0; k < ((s - 1) >> 5); ++k) sticky |= mag[k] != 0;
+      for (int k = 0; k < ((s - 1) >> 5); ++k) sticky |= magw(k) != 0;
       int sb = (s - 1) & 31;
-      if (sb) sticky |= (mag[(s - 1) >> 5] & ((1u << sb) - 1u)) != 0;
+      if (sb) sticky |= (magw((s - 1) >> 5) & ((1u << sb) - 1u)) != 0;
       shift = s;
       if (e >= 0) {
         // gmpy2 mpz->float truncates: keep mant, no rounding

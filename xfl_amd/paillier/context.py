@@ -13,7 +13,7 @@ from typing import Optional
 
 from .utils import getprimeover, invert
 
-SUPPORTED_DEVICE_BITS = (2048, 3072, 4096)
+SUPPORTED_DEVICE_BITS = (2048, 3072, 4096, 8192)
 
 
 def device_key_bits(n):
