@@ -50,8 +50,14 @@ def run(bits, steps):
     te = _timed(lambda: _encrypt_f64(nat, L, dk, x, 7, m, ex, st, rnd, ct, 1, s), steps)
     td = _timed(lambda: nat.check(L.xhe_decrypt(dk.handle, ct.data_ptr(), N, m2.data_ptr(), s), "decrypt"), steps)
     _sync()
+    # SURVEY 8(d) model: 2 nwin table products of s = K/32 limbs at 2s^2+s
+    # MACs (bench.py's roofline.achieved), over the measured v_mad peak
+    s_ = bits // 32
+    macs = 2 * (-(-dk.rand_bits // WIN_BY_BITS[bits])) * (2 * s_ * s_ + s_)
     out = {"key_bits": bits, "elements": N, "fixed_base_window_bits": WIN_BY_BITS[bits],
            "encrypts_per_s": N / te, "decrypts_per_s": N / td,
+           "alg_macs_per_encrypt": macs, "encrypt_tmac_per_s": N / te * macs / 1e12,
+           "encrypt_roofline_frac": N / te * macs / 39.3216e12,
            "roundtrip_bit_exact": bool(torch.equal(m, m2)), "key_setup_s": tk}
     del dk
     torch.cuda.empty_cache()

@@ -867,7 +867,13 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
   using MP2 = typename Sh::MP2;
   using MP = typename Sh::MP;
   const int pin = dec_tpi_override();
-  const int tpi = pin ? pin : count <= kDecRowMax ? 16 : count <= kDecQuadMax ? 4 : 1;
+  // Multi-lane key sizes take the 4-lane shape for every larger batch: at 3072
+  // bits the 2-lane batch shape (55 limbs per lane) decrypted 25.5 k/s where
+  // 4096 bits in 4 lanes reach 133 k/s (profiles/r1/keysizes/).
+  const int tpi = pin ? pin
+                      : count <= kDecRowMax                        ? 16
+                      : (count <= kDecQuadMax || MP2::TPI > 1) ? 4
+                                                                   : 1;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t *xrows = nullptr, *mrows = nullptr;
   HIPCHK(hipMallocAsync((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
