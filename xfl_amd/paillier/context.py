@@ -78,7 +78,9 @@ class PaillierContext(object):
             x = secrets.SystemRandom().getrandbits(n.bit_length())
             x |= 1 << (n.bit_length() - 1)
             h = -pow(x, 2)
-            h_pow_n = pow(h, n, n * n)
+            from . import _gmp
+            n2 = n * n
+            h_pow_n = _gmp.powmod(h % n2, n, n2) if _gmp.available() else pow(h, n, n2)
             return PaillierContext().init(p, q, djn_h_pow_n=h_pow_n)
         return PaillierContext().init(p, q)
 

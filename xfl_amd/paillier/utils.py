@@ -79,7 +79,11 @@ def is_probable_prime(n, rounds=32, rng=None):
 
 
 def next_prime(x, rng=None):
-    """Smallest probable prime > x (gmpy2.next_prime semantics)."""
+    """Smallest probable prime > x (gmpy2.next_prime semantics): GMP's
+    mpz_nextprime when libgmp is present (what gmpy2 calls), else Miller-Rabin."""
+    from . import _gmp
+    if _gmp.available() and x >= 0:
+        return _gmp.next_prime(int(x))
     n = x + 1
     if n <= 2:
         return 2
