@@ -119,3 +119,24 @@ def test_djn_encrypt_both_shapes():
             ok = O.derive_private(p, q, h)
             for i in (0, SMALL - 1, nbig - 1):
                 assert big[i] == O.encrypt_m(ok, ms[i], rs[i])
+
+
+@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+def test_private_nodjn_encrypt_closed_form(fx):
+    """Private-key non-DJN encryption (r^ep mod p^2, r^eq mod q^2, CRT;
+    paillier.py:214-230) equals the closed form (1 + n m) r^n mod n^2 —
+    at 3072 bits it runs in the 4-lane shape, not the 2-lane batch shape."""
+    from xfl_amd import _native as nat
+    k = load_fixture(fx)["key"]
+    p, q = hx(k["p"]), hx(k["q"])
+    n = p * q
+    n2 = n * n
+    dk = nat.DeviceKey(int(fx.split("_")[1]), n, p, q, None, device=0)
+    rng = random.Random(11)
+    count = 2000
+    ms = [rng.randrange(n) for _ in range(count)]
+    rs = [rng.randrange(1, n) for _ in range(count)]
+    ct = nat.words_to_ints(dk.encrypt_words(nat.ints_to_words(ms, dk.nw), nat.ints_to_words(rs, dk.rand_words)))
+    for i in list(range(4)) + [count - 1]:
+        assert ct[i] == (1 + n * ms[i]) * pow(rs[i], n, n2) % n2, i
+    assert nat.words_to_ints(dk.decrypt_words(nat.ints_to_words(ct, dk.n2w))) == ms

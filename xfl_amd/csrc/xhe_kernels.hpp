@@ -49,6 +49,8 @@ struct KeyDev {
   const uint32_t *nR2C_p2X, *nR2C_q2X;  // n * C * R'^2 mod P^2
   const uint32_t *R1C_p2X, *R1C_q2X;    // C * R' mod P^2
   const uint32_t* nR2_q2;     // n * R^2 mod q^2
+  const uint32_t* nR2_p2L;    // n * R_L^2 mod p^2 / q^2 in the 4-lane (p2L) shape
+  const uint32_t* nR2_q2L;
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
   const uint32_t* q2_lim;     // q^2 (MP2 limbs)
   const uint32_t* p2x4_lim;   // 4 p^2 (MP2 limbs)
@@ -903,14 +905,18 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_pub(KeyDev key, const uint32_t
   }
 }
 
-template <class MP2>
+// SHAPE 0: the batch shape (key.p2/q2); 1: the 4-lane shape (key.p2L/q2L),
+// for key sizes whose batch shape spills in this exponentiation (3072 bits:
+// 55 limbs per lane). Rows are written RS4 limbs apart for k_crt_enc.
+template <class MP2, int SHAPE = 0, int RS4 = MP2::S4>
 __global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t* __restrict__ Np2,
                                                       const uint32_t* __restrict__ Nq2,
                                                       const uint32_t* __restrict__ m_words,
                                                       const uint32_t* __restrict__ r_words, int rw, int64_t count,
                                                       uint32_t* __restrict__ rows, uint32_t* __restrict__ ws) {
   const int prime = blockIdx.y;
-  const ModDev& md = prime ? key.q2 : key.p2;
+  const ModDev& md = SHAPE ? (prime ? key.q2L : key.p2L) : (prime ? key.q2 : key.p2);
+  const uint32_t* nR2 = SHAPE ? (prime ? key.nR2_q2L : key.nR2_p2L) : (prime ? key.nR2_q2 : key.nR2_p2);
   const int64_t G_total = (int64_t)gridDim.x * blockDim.x / MP2::TPI;
   const int64_t gid0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   const int st = (int)G_total;
@@ -926,10 +932,10 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t
     MP2 M;
     M.init(prime ? Nq2 : Np2, md.n0inv);
     uint32_t b[MP2::L];
-    nodjn_core(M, b, md, prime ? key.nR2_q2 : key.nR2_p2, m_words + (size_t)e * key.nw, key.nw,
+    nodjn_core(M, b, md, nR2, m_words + (size_t)e * key.nw, key.nw,
                r_words + (size_t)e * rw, rw, prime ? key.eq_words : key.ep_words, key.nw,
                prime ? key.eq_bits : key.ep_bits, tab, tab + 16 * rs, tab + 17 * rs, st, sq_lds);
-    M.store_strided(b, rows + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+    M.store_strided_n(b, rows + (size_t)prime * 2 * RS4 * count + e, (int)count, RS4);
   }
 }
 
