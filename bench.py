@@ -87,15 +87,16 @@ def table_bytes(bits, win):
     ceil(rand_bits/win) windows x 2^win rows x S4 words per prime, S4 the
     radix-2^28 limb count of P^2 rounded up to 4."""
     rand_bits = bits // 2
-    s4 = -(-(-(-(bits + 4) // 28)) // 4) * 4
+    s4 = {2048: 76, 3072: 112, 4096: 152, 8192: 304}[bits]  # xhe.hip Shape<K>::MP2::S4
     return 2 * -(-rand_bits // win) * (1 << win) * s4 * 4
 
 
 def pick_window(bits, free_bytes, margin=16 << 30):
-    for w in (23, 22):
+    """Widest window (<= 23) whose tables leave `margin` of HBM free."""
+    for w in range(23, 11, -1):
         if table_bytes(bits, w) + margin <= free_bytes:
             return w
-    return 20
+    return 12
 
 
 def pmc_traffic(win, n):
