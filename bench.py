@@ -82,13 +82,15 @@ def cpu_baseline(bits, seconds, cores):
                       f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
 
 
+TABLE_ROW_BYTES = {2048: 304, 3072: 448, 4096: 608, 8192: 1216}  # S4 words x 4 (xhe.hip Shape<K>::MP2::S4)
+
+
 def table_bytes(bits, win):
     """Device bytes of the two fixed-base tables (xhe_key_create, include/xhe.h):
     ceil(rand_bits/win) windows x 2^win rows x S4 words per prime, S4 the
     radix-2^28 limb count of P^2 rounded up to 4."""
     rand_bits = bits // 2
-    s4 = {2048: 76, 3072: 112, 4096: 152, 8192: 304}[bits]  # xhe.hip Shape<K>::MP2::S4
-    return 2 * -(-rand_bits // win) * (1 << win) * s4 * 4
+    return 2 * -(-rand_bits // win) * (1 << win) * TABLE_ROW_BYTES[bits]
 
 
 def pick_window(bits, free_bytes, margin=16 << 30):
@@ -104,7 +106,7 @@ def pmc_traffic(win, n):
     (tools/profile_box.sh -> tools/pmc_traffic.py), when they were taken on
     this configuration; else None. Counters cannot be read inside this run
     (rocprofv3 --pmc is its own pass)."""
-    path = os.path.join(ROOT, "profiles", "r1", "k_djn_pow_pmc.json")
+    path = os.path.join(ROOT, "profiles", "r2", "k_djn_pow_pmc.json")
     try:
         with open(path) as f:
             rec = json.load(f)
@@ -220,6 +222,32 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
     return out
 
 
+def host_cores():
+    """(cores this process may use, cores the machine has): the cgroup CPU
+    quota or the affinity mask, whichever is smaller - on the GPU box
+    os.cpu_count() shows the whole machine, of which a job gets a share."""
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return usable, total
+
+
+def cpu_baselines(bits, seconds):
+    """cpu_baseline on every usable host core, plus the 1-core leg."""
+    usable, total = host_cores()
+    rec = cpu_baseline(bits, seconds, usable)
+    one = cpu_baseline(bits, max(2.0, seconds / 2), 1)
+    rec["machine_cpu_count"] = total
+    rec["single_core"] = {"value": one["value"], "unit": one["unit"], "cores": 1, "sample": one["sample"]}
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,11 +263,20 @@ def main():
     ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # one process per GPU, started here before anything touches the GPU
+        from xfl_amd.shard import spawn_local_ranks
+        sys.exit(spawn_local_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; they must agree")
+
     import torch
     import torch.distributed as dist
     from xfl_amd import _native as nat
+    from xfl_amd.shard import GatherPipeline, shard_parity
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -263,52 +300,32 @@ def main():
     ex = torch.empty(N, dtype=torch.int32, device="cuda")
     st = torch.empty(N, dtype=torch.int32, device="cuda")
     rnd = torch.empty((N, dk.rand_words), dtype=torch.int32, device="cuda")
-    # N > 1: ciphertext shards and gathered vectors are double-buffered so the
-    # all-gather of step i (RCCL's stream) overlaps the kernels of step i+1
-    nb = 2 if world > 1 else 1
-    cts = [torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda") for _ in range(nb)]
-    gathered = [torch.empty((world * N, dk.n2w), dtype=torch.int32, device="cuda") for _ in range(nb)] \
-        if world > 1 else None
-    pending = [None] * nb
     seed32 = os.urandom(32)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(i):
-        b = i % nb
-        if pending[b] is not None:  # the gather still reading cts[b] must finish before it is rewritten
-            pending[b].wait()
-            pending[b] = None
-        ct = cts[b]
+    def encrypt_shard(i, ct):
         nat.check(L.xhe_encode_f64(dk.handle, x.data_ptr(), N, 7, 0, 0, m.data_ptr(), ex.data_ptr(),
                                    st.data_ptr(), stream), "encode")
         nat.check(L.xhe_rand(dk.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
         nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
-        if world > 1:
-            pending[b] = dist.all_gather_into_tensor(gathered[b], ct, async_op=True)
-        return ct
 
-    def drain():
-        for b in range(nb):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
-
+    pipe = GatherPipeline(encrypt_shard, N, dk.n2w, world=world, rank=rank, device="cuda")
     last = 1_000_000 + max(args.warmup, 1) - 1  # the parity check below needs one finished step
     for i in range(1_000_000, last + 1):
-        ct = step(i)
-    drain()
+        pipe.step(i)
+    pipe.drain()
     torch.cuda.synchronize()
     # parity spot check of this rank's output against the oracle (not timed)
     from oracle import paillier_oracle as O
     okey = O.derive_private(p, q, h)
     idx = [0, 1, N // 2, N - 1]
-    xs = x[idx].cpu().numpy()
-    got = nat.words_to_ints(ct[idx].cpu().numpy().view(np.uint32))
-    rs = nat.words_to_ints(rnd[idx].cpu().numpy().view(np.uint32))
-    parity_ok = all(O.encrypt_m(okey, O.encode_element(okey, float(xv), 7)[0], rv) == cv
-                    for xv, rv, cv in zip(xs, rs, got))
-    if world > 1:  # the reassembled vector holds this rank's shard at its offset
-        parity_ok = parity_ok and bool(torch.equal(gathered[last % nb][rank * N:(rank + 1) * N], ct))
+    xs = x.cpu().numpy()
+    rnd_h = rnd.cpu().numpy().view(np.uint32)
+
+    def expected(i):
+        return O.encrypt_m(okey, O.encode_element(okey, float(xs[i]), 7)[0], nat.words_to_ints(rnd_h[i]))
+
+    parity_ok = shard_parity(pipe.shard(last), pipe.vector(last) if world > 1 else None, rank, idx, expected)
 
     L.xhe_profile(1)
     if world > 1:
@@ -319,8 +336,8 @@ def main():
     t0 = time.time()
     ev0.record()
     for i in range(args.steps):
-        ct = step(i)
-    drain()
+        ct = pipe.step(i)
+    pipe.drain()
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -360,16 +377,16 @@ def main():
             "roofline": {"bound": "valu-int", "achieved": achieved, "peak": PEAK_MAC_PER_S / 1e12,
                          "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": kname, "kernel_avg_ms": pow_avg_s * 1e3,
-                         "alg_macs_per_element": w_pow},
+                         "alg_macs_per_element": w_pow,
+                         "alg_table_bytes_per_launch": N * 2 * -(-dk.rand_bits // args.win) * TABLE_ROW_BYTES[bits]},
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,
         }
         if not args.no_ops:
             rec["ops"] = measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, (p, q, n, h))
         if not args.no_cpu_baseline:
-            cores = min(os.cpu_count() or 1, 16)
-            rec["cpu_baseline"] = cpu_baseline(bits, args.cpu_seconds, cores)
-        print(json.dumps(rec))
+            rec["cpu_baseline"] = cpu_baselines(bits, args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

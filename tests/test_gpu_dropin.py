@@ -83,17 +83,24 @@ def test_histogram_groupby_bit_exact():
 @pytest.mark.parametrize("fx", FIXTURES)
 def test_decrypt_matches_reference(fx):
     from xfl_amd.paillier import Paillier
+    from xfl_amd.paillier.encoder import int_to_float_gmpy
     g = load_fixture(fx)
     priv, pub = _ctxs(g)
-    for case in ("priv_f32_p7", "pub_f64_none_max-60", "priv_packed_p0"):
+    for case in ("priv_f32_p7", "pub_f64_none_max-60", "priv_packed_p0", "pub_i32_none", "priv_edge_p7_noobf"):
         enc = g["encrypt"][case]
         dec = g["decrypt"][case]
         c = _cts(priv, enc)
         f32 = Paillier.decrypt(priv, c, dtype="float", num_cores=1)
         assert [float(v).hex() for v in f32.astype(np.float64)] == dec["float32"]
         org = Paillier.decrypt(priv, c, num_cores=1, out_origin=True)
-        for v, want in zip(org, dec["origin_f64"]):
-            assert (float(v).hex() if isinstance(v, float) else float(v).hex()) == want or isinstance(v, int)
+        want_m = [hx(m) for m in dec["m"][len(dec["m"]) - len(enc["raw"]):]]
+        n = priv.n
+        for v, want, m, e in zip(org, dec["origin_f64"], want_m, enc["exp"]):
+            if e >= 0:  # integer decode: out_origin is the exact signed integer (an mpz in the reference)
+                assert isinstance(v, int) and v == (m - n if m >= priv.min_value_for_negative else m) << e
+                assert int_to_float_gmpy(v).hex() == want  # the reference's float(mpz), truncating
+            else:
+                assert isinstance(v, float) and v.hex() == want
 
 
 def test_wire_roundtrip_with_reference_pickles():

@@ -59,7 +59,13 @@ def test_malformed_input_rejected():
     from xfl_amd.paillier import wire
     raws, exps = _vals(3)
     b = wire.encode(raws, exps, (len(raws),), 129)
-    for bad in (b[:-7], b"\x80\x04garbage", pickle.dumps([1, 2, 3]), pickle.dumps(np.arange(4))):
+    crafted = (b"K\x01a.",                                  # APPEND with no list under it (was a heap write)
+               b"K\x01K\x02s.",                             # SETITEM with no dict
+               b")K\x01K\x02s.",                            # SETITEM into a tuple
+               b"\x8e" + b"\xff" * 7 + b"\x7f" + b"x",       # BINBYTES8 of length INT64_MAX (pos + k overflow)
+               b"\x8d" + b"\xf0" + b"\xff" * 6 + b"\x7f" + b"x",
+               b"K\x01r\xff\xff\xff\x03.")                  # memo index far beyond the input size
+    for bad in (b[:-7], b"\x80\x04garbage", pickle.dumps([1, 2, 3]), pickle.dumps(np.arange(4))) + crafted:
         with pytest.raises(ValueError):
             wire.decode(bad, 129)
     with pytest.raises(ValueError):  # value wider than the word budget

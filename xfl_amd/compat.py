@@ -46,15 +46,33 @@ def gmpy2_from_binary(b):
     return -mag if b[1] == 0x02 else mag
 
 
+# Globals a ciphertext / context / RawCiphertext payload may name
+# (paillier.py:244-271, context.py:152-168): numpy's ndarray reduce (numpy 1.x
+# and 2.x module paths), numpy scalars (an exponent can be an np.int32 taken
+# from np.frexp), protocol-0/1 object reconstruction and plain builtins.
+# Anything else raises instead of importing: peer bytes are untrusted.
+_ALLOWED = {
+    ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+    ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+    ("numpy", "ndarray"), ("numpy", "dtype"),
+    ("copyreg", "_reconstructor"), ("copy_reg", "_reconstructor"),
+    ("builtins", "object"), ("__builtin__", "object"),
+    ("builtins", "int"), ("builtins", "float"), ("builtins", "tuple"), ("builtins", "list"),
+    ("builtins", "dict"), ("builtins", "bytes"), ("builtins", "str"), ("builtins", "complex"),
+    ("_codecs", "encode"),  # protocol < 3 pickles of bytes
+}
+
+
 class _Unpickler(pickle.Unpickler):
     def find_class(self, module, name):
-        if module == "gmpy2" and name in ("from_binary", "_mpmath_create"):
-            if name == "from_binary":
-                return gmpy2_from_binary
+        if module == "gmpy2" and name == "from_binary":
+            return gmpy2_from_binary
         if module == _REF_MOD and name == "RawCiphertext":
             from .paillier.paillier import RawCiphertext
             return RawCiphertext
-        return super().find_class(module, name)
+        if (module, name) in _ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"global {module}.{name} is not allowed in a Paillier payload")
 
 
 def dumps(obj) -> bytes:

@@ -417,8 +417,8 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
         g0 -= g1;
       }
       xa >>= 1;
-      f1 <<= 1;
-      g1 <<= 1;
+      f1 *= 2;  // |f1|, |g1| <= 2^31: no overflow (a shift of a negative value would be UB)
+      g1 *= 2;
     }
     if (lin_shift(f0, a, g0, b, na)) {
       f0 = -f0;

@@ -208,7 +208,7 @@ struct Machine {
   }
   [[noreturn]] void bad(const char* why) { throw std::runtime_error(std::string("wire decode: ") + why); }
   const uint8_t* take(int64_t k) {
-    if (k < 0 || pos + k > len) bad("truncated");
+    if (k < 0 || k > len - pos) bad("truncated");  // no pos + k: k comes from an 8-byte field
     const uint8_t* r = p + pos;
     pos += k;
     return r;
@@ -275,8 +275,17 @@ struct Machine {
     if (v.off >= 0) return (size_t)v.n == l && memcmp(p + v.off, lit, l) == 0;
     return v.s == lit;
   }
+  // the container an APPEND(S)/SETITEM(S)/BUILD writes into: the stack top,
+  // which must exist and be of the right kind
+  Val& target(Val::Kind want, const char* what) {
+    if (stack.empty()) bad(what);
+    Val& t = arena[stack.back()];
+    if (t.k != want) bad(what);
+    return t;
+  }
   void put_memo(uint64_t i, int32_t v) {
-    if (i > (1u << 26)) bad("memo index");
+    // a memo index never exceeds the number of values created (<= input bytes)
+    if (i > (uint64_t)len || i > (1u << 26)) bad("memo index");
     if (memo.size() <= i) memo.resize(i + 1, -1);
     memo[i] = v;
   }
@@ -316,27 +325,26 @@ struct Machine {
         case '}': { Val v; v.k = Val::DICT; stack.push_back(make(v)); break; }
         case 'a': {
           int32_t x = pop();
-          arena[stack.back()].items.push_back(x);
+          target(Val::LIST, "append target").items.push_back(x);
           break;
         }
         case 'e': {
           const auto& xs = pop_mark();
-          if (stack.empty()) bad("appends target");
-          auto& l = arena[stack.back()].items;
+          auto& l = target(Val::LIST, "appends target").items;
           l.insert(l.end(), xs.begin(), xs.end());
           break;
         }
         case 's': {
           int32_t v = pop(), k = pop();
-          auto& d = arena[stack.back()].items;
+          auto& d = target(Val::DICT, "setitem target").items;
           d.push_back(k);
           d.push_back(v);
           break;
         }
         case 'u': {
           const auto& xs = pop_mark();
-          if (stack.empty() || xs.size() % 2) bad("setitems");
-          auto& d = arena[stack.back()].items;
+          if (xs.size() % 2) bad("setitems");
+          auto& d = target(Val::DICT, "setitems target").items;
           d.insert(d.end(), xs.begin(), xs.end());
           break;
         }
@@ -386,8 +394,7 @@ struct Machine {
         }
         case 'b': {
           int32_t st = pop();
-          if (stack.empty()) bad("build target");
-          arena[stack.back()].state = st;
+          target(Val::OBJ, "build target").state = st;
           break;
         }
         case 0x94: if (stack.empty()) bad("memoize"); put_memo(memo.size(), stack.back()); break;

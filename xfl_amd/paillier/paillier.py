@@ -384,13 +384,12 @@ class Paillier(object):
             if not all(isinstance(c, PaillierCiphertext) for c in flat):
                 raise TypeError("Unsupported raw ciphertext type")
             if len(flat):
+                # re-randomise the caller's objects in place (c.obfuscate() per
+                # element in the reference), one batched call
                 ctx = flat[0].context
                 raws = ops.obfuscate(ctx, raws_of(list(flat)))
-                out = np.empty(len(flat), dtype=object)
-                for i, (c, r) in enumerate(zip(flat, raws)):
-                    out[i] = PaillierCiphertext(c.context, r, c.exponent)
-                from .array import PaillierArray
-                return out.reshape(ciphertext.shape).view(PaillierArray)
+                for c, r in zip(flat, raws):
+                    c._set_raw(r)
             return ciphertext
         elif isinstance(ciphertext, PaillierCiphertext):
             return ciphertext.obfuscate()

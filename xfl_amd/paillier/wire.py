@@ -11,7 +11,7 @@ import numpy as np
 
 from .. import _native as nat
 
-_MAX_WORDS = 256  # n^2 of a 4096-bit key
+_MAX_WORDS = 512  # n^2 of an 8192-bit key, the largest device key size (context.SUPPORTED_DEVICE_BITS)
 
 
 def _vp(a):
