@@ -219,6 +219,28 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
                                                            None), "decrypt_host"), reps=2)
     out["decrypt_decode_host_buffers_per_s"] = nh / t
     out["host_roundtrip_max_abs_err"] = float(np.max(np.abs(f64 - xh)))
+    # the same through the drop-in API (what XFL's operators call): the label
+    # trainer's Paillier.encrypt(float32[]) -> Paillier.serialize, and the
+    # receiving side's ciphertext_from -> Paillier.decrypt
+    # (logistic_regression/label_trainer.py:193-199, 258); the context uses
+    # this run's key handle (same tables)
+    from xfl_amd.paillier import Paillier, PaillierContext
+    ctx = PaillierContext().init(p_, q_, djn_h_pow_n=h_)
+    ctx._dev = {dk.device: dk}
+    x32 = xh.astype(np.float32)
+    wire = {}
+
+    def enc_ser(comp):
+        wire[comp] = Paillier.serialize(Paillier.encrypt(ctx, x32, precision=7), compression=comp)
+    t = _timed(lambda: enc_ser(False), reps=2)
+    out["dropin_encrypt_serialize_per_s"] = nh / t
+    t = _timed(lambda: Paillier.decrypt(ctx, Paillier.ciphertext_from(None, wire[False], compression=False)), reps=2)
+    out["dropin_deserialize_decrypt_per_s"] = nh / t
+    back = Paillier.decrypt(ctx, Paillier.ciphertext_from(None, wire[False], compression=False))
+    out["dropin_roundtrip_max_abs_err"] = float(np.max(np.abs(back - x32)))
+    t = _timed(lambda: enc_ser(True), reps=1)
+    out["dropin_encrypt_serialize_zstd_per_s"] = nh / t
+    out["wire_bytes_per_ciphertext"] = len(wire[False]) / nh
     return out
 
 

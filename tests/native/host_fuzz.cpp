@@ -138,6 +138,40 @@ static void roundtrip(std::mt19937_64& rng) {
   }
 }
 
+// Our own encoder's output: the fast decode path must accept it and agree
+// with the general pickle machine; then it is fuzzed like the other seeds.
+static void own_format(std::mt19937_64& rng) {
+  const int64_t counts[] = {0, 1, 5, 999, 1000, 1001, 2500};
+  for (int64_t count : counts) {
+    const int n2w = 128;
+    std::vector<uint32_t> ct((size_t)std::max<int64_t>(count, 1) * n2w);
+    std::vector<int32_t> ex((size_t)std::max<int64_t>(count, 1));
+    for (auto& w : ct) w = (uint32_t)rng();
+    for (int64_t i = 0; i < count; ++i) {
+      ex[i] = (int32_t)(rng() % 3 == 0 ? rng() : rng() % 300);
+      int top = (int)(rng() % n2w);  // varying value lengths, incl. LONG1/LONG4 and zero
+      for (int k = top; k < n2w; ++k) ct[(size_t)i * n2w + k] = 0;
+    }
+    int64_t shape[2] = {count, 1};
+    for (int threads : {1, 3}) {
+      int64_t need = xhe::wire::encode(ct.data(), ex.data(), count, n2w, shape, 2, nullptr, 0, threads);
+      Bytes out((size_t)need);
+      xhe::wire::encode(ct.data(), ex.data(), count, n2w, shape, 2, out.data(), need, threads);
+      const int64_t cap = std::max<int64_t>(count, 1);
+      std::vector<uint32_t> a((size_t)cap * n2w), b((size_t)cap * n2w);
+      std::vector<int32_t> ea(cap), eb(cap);
+      int64_t sa[8], sb[8];
+      int na = 0, nb = 0;
+      int64_t ka = xhe::wire::decode_own(out.data(), need, n2w, a.data(), ea.data(), cap, sa, &na);
+      int64_t kb = xhe::wire::decode_general(out.data(), need, n2w, b.data(), eb.data(), cap, sb, &nb);
+      if (ka != count || kb != count || na != 2 || nb != 2 || sa[0] != count || sb[0] != count) std::abort();
+      if (count && (a != b || ea != eb)) std::abort();
+      if (count && std::memcmp(a.data(), ct.data(), (size_t)count * n2w * 4)) std::abort();
+      if (count > 0 && count <= 5) fuzz_seed(out, rng);
+    }
+  }
+}
+
 static xhe::BigU from_hex(const std::string& h) {
   std::vector<uint32_t> w((h.size() + 7) / 8 + 1, 0);
   int bit = 0;
@@ -209,6 +243,7 @@ int main(int argc, char** argv) {
   }
   crafted();
   roundtrip(rng);
+  own_format(rng);
   std::printf("seeds %ld decoded %ld rejected %ld\n", seeds_ok, g_ok, g_rejected);
   return 0;
 }

@@ -1,0 +1,129 @@
+"""CPU: the drop-in's host logic against the reference's golden vectors, with
+the eight device entry points of xfl_amd.paillier.ops replaced by the oracle
+(tests/oracle_ops.py). The same checks run on the real kernels in
+tests/test_gpu_dropin.py; this copy exercises PaillierArray's flat buffers,
+broadcasting, scalar encoding, alignment, sign branches, decode dtype paths
+and the wire codec on any machine (2048-bit fixtures: pure-Python modexp)."""
+import pytest
+
+from tests import dropin_cases as C
+from tests import oracle_ops
+
+HOST_FIXTURES = ["paillier_2048_djn.json", "paillier_2048_nodjn.json"]
+
+
+@pytest.fixture(autouse=True)
+def _oracle_ops(monkeypatch):
+    oracle_ops.install(monkeypatch)
+
+
+@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_ops_bit_exact(fx, vectorized):
+    C.ops_bit_exact(fx, vectorized)
+
+
+def test_histogram_groupby_bit_exact():
+    C.histogram_groupby(HOST_FIXTURES[0])
+
+
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_decrypt_matches_reference(fx):
+    C.decrypt_matches_reference(fx)
+
+
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_wire_roundtrip_with_reference_pickles(fx):
+    C.wire_roundtrip(fx)
+
+
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_array_protocol(fx):
+    C.array_protocol(fx)
+
+
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_encrypt_decrypt_shapes(fx):
+    C.encrypt_decrypt_shapes(fx)
+
+
+def test_sharded_slices_cover_the_batch(monkeypatch):
+    """ops.sharded: contiguous slices, one per shard device, small batches on
+    the first device only, devices taken from $XHE_DEVICES / num_cores."""
+    import threading
+
+    from xfl_amd.paillier import ops
+    from xfl_amd.paillier.context import PaillierContext
+
+    class Ctx:
+        def __init__(self):
+            self.keys = []
+
+        shard_devices = staticmethod(PaillierContext.shard_devices)
+
+        def device_key(self, d):
+            self.keys.append(d)
+            return d
+
+    monkeypatch.setattr(ops, "MIN_SHARD", 10)
+    for spec, count, want_k in (("0,1,2,3", 1000, 4), ("0,1,2,3", 25, 2), ("5", 1000, 1), ("0,0,0", 31, 3),
+                                ("0,1", 9, 1)):
+        monkeypatch.setenv("XHE_DEVICES", spec)
+        ctx = Ctx()
+        seen = []
+        lock = threading.Lock()
+
+        def body(dk, lo, hi):
+            with lock:
+                seen.append((dk, lo, hi))
+        ops.sharded(ctx, count, body)
+        seen.sort(key=lambda t: t[1])
+        assert len(seen) == want_k
+        assert seen[0][1] == 0 and seen[-1][2] == count
+        assert all(seen[i][2] == seen[i + 1][1] for i in range(len(seen) - 1))
+        devs = [int(d) for d in spec.split(",")]
+        assert [s[0] for s in seen] == devs[:want_k]
+    monkeypatch.delenv("XHE_DEVICES")
+    monkeypatch.setattr("xfl_amd._native.visible_devices", lambda: 8)
+    assert PaillierContext.shard_devices(-1) == list(range(8))
+    assert PaillierContext.shard_devices(3) == [0, 1, 2]
+    assert PaillierContext.shard_devices(1) == [0]
+
+
+def test_table_window_policy(monkeypatch):
+    """The fixed-base window follows the key's encrypted volume (16 -> 20 ->
+    22) as far as free HBM allows; pinned by set_device_window / $XHE_WIN_BITS;
+    public and non-DJN keys carry no tables."""
+    import xfl_amd._native as nat
+    from tests.conftest import load_fixture
+    built = []
+
+    class FakeKey:
+        def __init__(self, bits, n, p=None, q=None, h=None, device=0, win_bits=0):
+            self.win_bits = win_bits if (p is not None and h) else 0
+            built.append((device, self.win_bits))
+
+    monkeypatch.setattr(nat, "DeviceKey", FakeKey)
+    free = {"b": 200 << 30}
+    monkeypatch.setattr(nat, "device_free_bytes", lambda d=0: free["b"])
+    monkeypatch.delenv("XHE_WIN_BITS", raising=False)
+    priv, pub = C.ctxs(load_fixture("paillier_2048_djn.json"))
+    assert priv.device_key().win_bits == 16
+    priv.note_encrypt_volume(7_000_000)
+    assert priv.device_key().win_bits == 16 and len(built) == 1
+    priv.note_encrypt_volume(2_000_000)
+    assert priv.device_key().win_bits == 20
+    priv.note_encrypt_volume(100_000_000)
+    free["b"] = 100 << 30  # 2 x 59.9 GB + 32 GiB margin does not fit next to the win-20 tables' 33 GB
+    assert priv.device_key().win_bits == 20
+    free["b"] = 200 << 30
+    assert priv.device_key().win_bits == 22
+    assert [w for _, w in built] == [16, 20, 22]
+    priv.set_device_window(18)
+    assert priv.device_key().win_bits == 18
+    monkeypatch.setenv("XHE_WIN_BITS", "12")
+    priv.set_device_window(None)
+    assert priv.device_key().win_bits == 12
+    assert pub.device_key().win_bits == 0
+    nodjn, _ = C.ctxs(load_fixture("paillier_2048_nodjn.json"))
+    assert nodjn.device_key().win_bits == 0

@@ -15,104 +15,41 @@ from tests.conftest import FIXTURES, fl, hx, load_fixture
 pytestmark = pytest.mark.gpu
 
 
-def _ctxs(g):
-    from xfl_amd.paillier import PaillierContext
-    k = g["key"]
-    h = hx(k["h_pow_n"]) if k["djn_on"] else None
-    priv = PaillierContext().init(hx(k["p"]), hx(k["q"]), djn_h_pow_n=h)
-    return priv, priv.to_public()
-
-
-def _cts(ctx, d):
-    from xfl_amd.paillier import PaillierCiphertext
-    return np.array([PaillierCiphertext(ctx, hx(r), e) for r, e in zip(d["raw"], d["exp"])], dtype=object)
-
-
-def _raw(arr):
-    return [c.raw_ciphertext for c in np.asarray(arr, dtype=object).reshape(-1)], \
-        [c.exponent for c in np.asarray(arr, dtype=object).reshape(-1)]
+from tests import dropin_cases as C
 
 
 @pytest.mark.parametrize("vectorized", [False, True])
 @pytest.mark.parametrize("fx", FIXTURES)
 def test_ops_bit_exact(fx, vectorized):
-    """vectorized=False: numpy's per-element object loop over PaillierCiphertext
-    operators; True: PaillierArray's batched kernels (segmented product,
-    batch inversion, multi-exponentiation matmul)."""
-    from xfl_amd.paillier import PaillierArray
-    g = load_fixture(fx)
-    priv, pub = _ctxs(g)
-    ops = g["ops"]
-    a = _cts(pub, ops["a"])
-    b = _cts(pub, ops["b"])
-    if vectorized:
-        a, b = PaillierArray(a), PaillierArray(b)
-    sc = [fl(s) if isinstance(s, str) else s for s in ops["mul_pub"]["scalar"]]
-    want = lambda name: ([hx(r) for r in ops[name]["raw"]], ops[name]["exp"])  # noqa: E731
-    assert _raw(a + b) == want("add")
-    assert _raw(a - b) == want("sub")
-    assert _raw(np.array([a[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_pub")
-    a_priv = _cts(priv, ops["a"])
-    assert _raw(np.array([a_priv[i] * sc[i] for i in range(len(a))], dtype=object)) == want("mul_priv")
-    if vectorized:
-        scv = np.array(sc, dtype=object)
-        assert _raw(a * scv) == want("mul_pub")
-        assert _raw(a + scv) == want("add_scalar")
-        assert _raw(scv - a) == want("rsub_scalar")
-    assert _raw(np.array([a[i] + sc[i] for i in range(len(a))], dtype=object)) == want("add_scalar")
-    assert _raw(np.array([sc[i] - a[i] for i in range(len(a))], dtype=object)) == want("rsub_scalar")
-    assert _raw(a / 4.0) == want("truediv")
-    assert _raw(np.array([np.sum(a)], dtype=object)) == want("sum_a")
-    assert _raw(np.array([sum(a)], dtype=object)) == want("sum_pyfold")
-    X = np.array([[fl(v) for v in row] for row in ops["matmul"]["X"]], dtype=np.float32)
-    assert _raw(np.matmul(a, X)) == want("matmul")
+    C.ops_bit_exact(fx, vectorized)
 
 
 def test_histogram_groupby_bit_exact():
-    import pandas as pd
-    g = load_fixture(FIXTURES[0])
-    priv, pub = _ctxs(g)
-    h = g["ops"]["hist"]
-    c = _cts(pub, h["ct"])
-    df = pd.DataFrame({"bin": h["bins"], "xfl_grad_hess": c})
-    agg = df.groupby(["bin"])["xfl_grad_hess"].agg(["count", "sum"])
-    assert list(agg["count"]) == h["count"]
-    assert _raw(np.array(list(agg["sum"]), dtype=object)) == ([hx(r) for r in h["sum"]["raw"]], h["sum"]["exp"])
+    C.histogram_groupby(FIXTURES[0])
 
 
 @pytest.mark.parametrize("fx", FIXTURES)
 def test_decrypt_matches_reference(fx):
-    from xfl_amd.paillier import Paillier
-    from xfl_amd.paillier.encoder import int_to_float_gmpy
-    g = load_fixture(fx)
-    priv, pub = _ctxs(g)
-    for case in ("priv_f32_p7", "pub_f64_none_max-60", "priv_packed_p0", "pub_i32_none", "priv_edge_p7_noobf"):
-        enc = g["encrypt"][case]
-        dec = g["decrypt"][case]
-        c = _cts(priv, enc)
-        f32 = Paillier.decrypt(priv, c, dtype="float", num_cores=1)
-        assert [float(v).hex() for v in f32.astype(np.float64)] == dec["float32"]
-        org = Paillier.decrypt(priv, c, num_cores=1, out_origin=True)
-        want_m = [hx(m) for m in dec["m"][len(dec["m"]) - len(enc["raw"]):]]
-        n = priv.n
-        for v, want, m, e in zip(org, dec["origin_f64"], want_m, enc["exp"]):
-            if e >= 0:  # integer decode: out_origin is the exact signed integer (an mpz in the reference)
-                assert isinstance(v, int) and v == (m - n if m >= priv.min_value_for_negative else m) << e
-                assert int_to_float_gmpy(v).hex() == want  # the reference's float(mpz), truncating
-            else:
-                assert isinstance(v, float) and v.hex() == want
+    C.decrypt_matches_reference(fx)
 
 
-def test_wire_roundtrip_with_reference_pickles():
-    from xfl_amd.paillier import Paillier, PaillierContext
-    g = load_fixture(FIXTURES[0])
-    priv, pub = _ctxs(g)
-    ctx = PaillierContext.deserialize_from(bytes.fromhex(g["ops"]["wire_ctx_pub"]))
-    assert ctx.n == pub.n
-    arr = Paillier.ciphertext_from(None, bytes.fromhex(g["ops"]["wire_a4"]), compression=False)
-    assert [c.raw_ciphertext for c in arr] == [hx(r) for r in g["ops"]["a"]["raw"][:4]]
-    back = Paillier.ciphertext_from(priv, Paillier.serialize(arr, compression=True), compression=True)
-    assert [c.raw_ciphertext for c in back] == [c.raw_ciphertext for c in arr]
+@pytest.mark.parametrize("fx", FIXTURES)
+def test_wire_roundtrip_with_reference_pickles(fx):
+    C.wire_roundtrip(fx)
+
+
+@pytest.mark.parametrize("fx", FIXTURES[:2])
+def test_array_protocol(fx):
+    C.array_protocol(fx)
+
+
+@pytest.mark.parametrize("fx", FIXTURES)
+def test_encrypt_decrypt_shapes(fx):
+    C.encrypt_decrypt_shapes(fx)
+
+
+def _ctxs(g):
+    return C.ctxs(g)
 
 
 # ---- ports of the reference's tolerance tests (test_paillier.py:24-296)

@@ -92,3 +92,44 @@ def test_merge_two_gloo_ranks_device_combine():
     for p in procs:
         p.join(timeout=60)
     assert all(res.values()), res
+
+
+# ------------------------------------------------------------ drop-in sharding
+def test_dropin_shards_over_devices(monkeypatch):
+    """num_cores / $XHE_DEVICES spread a batch over GPUs (the reference's
+    process pool, paillier.py:321-332,388-394): three shards on device 0 here,
+    each a host thread with its own slice of the output. Deterministic ops
+    equal the single-shard result bit for bit; encryptions decrypt back and
+    each shard draws its own randomness."""
+    from tests import dropin_cases as C
+    from xfl_amd.paillier import Paillier, ops
+    priv, pub = C.ctxs(load_fixture(FIXTURES[0]))
+    rng = np.random.default_rng(4)
+    x = (rng.random(3001) * 100 - 50).astype(np.float32)
+    y = rng.standard_normal(3001)
+    monkeypatch.setenv("XHE_DEVICES", "0")
+    c1 = Paillier.encrypt(priv, x, precision=7)
+    want_add = c1 + c1
+    want_mul = c1 * y
+    want_dec = Paillier.decrypt(priv, c1)
+    monkeypatch.setenv("XHE_DEVICES", "0,0,0")
+    monkeypatch.setattr(ops, "MIN_SHARD", 512)
+    calls = []
+    real = ops.sharded
+
+    def spy(ctx, count, body, num_cores=-1):
+        calls.append((count, len(ctx.shard_devices(num_cores))))
+        return real(ctx, count, body, num_cores)
+    monkeypatch.setattr(ops, "sharded", spy)
+    assert C.raw(c1 + c1) == C.raw(want_add)
+    assert C.raw(c1 * y) == C.raw(want_mul)
+    assert np.array_equal(Paillier.decrypt(priv, c1), want_dec)
+    c3 = Paillier.encrypt(pub, x, precision=7)
+    assert np.all(np.abs(Paillier.decrypt(priv, c3) - x) < 1e-4)
+    w = c3.words
+    third = len(x) // 3
+    assert len({w[i].tobytes() for i in (0, third, 2 * third)}) == 3
+    # same plaintext in every shard: distinct draws per shard
+    same = Paillier.encrypt(priv, np.full(3000, 1.25), precision=7)
+    assert len({bytes(r) for r in same.words}) == 3000
+    assert calls and all(d == 3 for _, d in calls)

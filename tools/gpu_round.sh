@@ -1,0 +1,38 @@
+#!/bin/bash
+# One gpurun call: GPU test suite, default bench line, optional rocprofv3
+# passes. Ordinary test failures (pytest exit 1) do not stop the script; a
+# crash, abort or time limit of any GPU step does (nothing else runs on the
+# GPU after it).
+#   tools/gpu_round.sh TAG [tests|bench|prof ...]   (default: tests bench)
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${1:-r2}
+shift
+STEPS=${*:-tests bench}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        ${PYTEST_ARGS} > "$OUT/gpu_tests.log" 2>&1
+      rc=$?
+      tail -3 "$OUT/gpu_tests.log"
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
+      ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit $?
+      cat "$OUT/smoke.log"
+      ;;
+    bench)
+      timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 3; }
+      cat "$OUT/bench.json"
+      ;;
+    prof)
+      bash tools/profile_box.sh "$TAG/prof" || exit $?
+      ;;
+    *)
+      echo "unknown step $s"; exit 2
+      ;;
+  esac
+done
+echo "gpu_round $TAG done"

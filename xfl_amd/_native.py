@@ -103,6 +103,17 @@ def lib():
     return _lib
 
 
+_ndev = None
+
+
+def visible_devices():
+    """GPUs visible to this process (cached)."""
+    global _ndev
+    if _ndev is None:
+        _ndev = max(1, int(lib().xhe_device_count()))
+    return _ndev
+
+
 def check(rc, what=""):
     if rc == XHE_OK:
         return
@@ -142,6 +153,26 @@ def ptr(a):
     return a.ctypes.data_as(_u32p)
 
 
+TABLE_ROW_WORDS = {2048: 76, 3072: 112, 4096: 152, 8192: 304}  # xhe.hip Shape<K>::MP2::S4
+
+
+def table_bytes(key_bits, win_bits):
+    """Device bytes of a DJN private key's two fixed-base tables: ceil(rand_bits
+    / win) windows x 2^win rows x S4 words per prime (rand_bits = K/2)."""
+    if not win_bits:
+        return 0
+    return 2 * -(-(key_bits // 2) // win_bits) * (1 << win_bits) * TABLE_ROW_WORDS[key_bits] * 4
+
+
+def device_free_bytes(device=0):
+    """Free HBM on `device` (None when it cannot be queried)."""
+    try:
+        import torch
+        return int(torch.cuda.mem_get_info(device)[0])
+    except Exception:
+        return None
+
+
 class DeviceKey:
     """Owns one xhe_key handle (device-resident key constants and tables)."""
 
@@ -166,6 +197,7 @@ class DeviceKey:
         self.private = bool(flags & 1)
         self.djn = bool(flags & 2)
         self.device = device
+        self.win_bits = (win_bits or int(os.environ.get("XHE_WIN_BITS", "0") or 16)) if self.private and self.djn else 0
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -13,6 +13,7 @@
 import ctypes
 import ctypes.util
 import io
+import threading
 import pickle
 import sys
 import types
@@ -108,14 +109,28 @@ def _lib():
     return _zstd
 
 
+_scratch = threading.local()
+
+
+def _dst(cap):
+    """per-thread output buffer, kept between calls (already paged in)"""
+    import numpy as np
+    buf = getattr(_scratch, "buf", None)
+    if buf is None or buf.shape[0] < cap:
+        buf = _scratch.buf = np.empty(cap, dtype=np.uint8)
+    return buf
+
+
 def compress(data: bytes, level: int = 3) -> bytes:
+    """zstd frame of data (the reference's zstd.compress, paillier.py:244-258):
+    one frame, content size in the header."""
     L = _lib()
     cap = L.ZSTD_compressBound(len(data))
-    dst = ctypes.create_string_buffer(cap)
-    n = L.ZSTD_compress(dst, cap, data, len(data), level)
+    dst = _dst(cap)
+    n = L.ZSTD_compress(dst.ctypes.data, cap, data, len(data), level)
     if L.ZSTD_isError(n):
         raise RuntimeError("zstd compression failed")
-    return dst.raw[:n]
+    return dst[:n].tobytes()
 
 
 def decompress(data: bytes) -> bytes:
@@ -123,8 +138,14 @@ def decompress(data: bytes) -> bytes:
     size = L.ZSTD_getFrameContentSize(data, len(data))
     if size >= (1 << 63):  # unknown / error
         raise RuntimeError("zstd frame without content size")
-    dst = ctypes.create_string_buffer(max(int(size), 1))
-    n = L.ZSTD_decompress(dst, int(size), data, len(data))
-    if L.ZSTD_isError(n):
+    if size < 2:  # bytes(0) / bytes(1) are shared singletons: never write into them
+        dst = ctypes.create_string_buffer(max(int(size), 1))
+        n = L.ZSTD_decompress(dst, int(size), data, len(data))
+        if L.ZSTD_isError(n):
+            raise RuntimeError("zstd decompression failed")
+        return ctypes.string_at(dst, n)
+    out = bytes(int(size))  # written in place: the frame fills it exactly
+    n = L.ZSTD_decompress(ctypes.cast(out, ctypes.c_void_p), int(size), data, len(data))
+    if L.ZSTD_isError(n) or n != size:
         raise RuntimeError("zstd decompression failed")
-    return dst.raw[:n]
+    return out

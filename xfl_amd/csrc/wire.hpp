@@ -19,10 +19,20 @@
 #include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace xhe {
 namespace wire {
+
+// f(0..T-1) on T threads (the calling thread runs part 0)
+template <class F>
+void run_parallel(int T, F&& f) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(f, t);
+  f(0);
+  for (auto& x : th) x.join();
+}
 
 struct Writer {
   uint8_t* out;
@@ -92,10 +102,7 @@ inline void put_long(Writer& w, const uint32_t* words, int nw) {
   for (int64_t i = have; i < nbytes; ++i) w.put((uint8_t)0);
 }
 
-// returns the byte count (writes only when it fits in cap)
-inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
-                      uint8_t* out, int64_t cap) {
-  Writer w{out, cap};
+inline void emit_header_a(Writer& w) {
   w.put(0x80);
   w.put(4);
   w.str("numpy.core.multiarray");
@@ -117,7 +124,9 @@ inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, in
   w.put('K');
   w.put(1);
   w.put('(');
-  for (int d = 0; d < ndim; ++d) w.binint64(shape[d]);
+}
+
+inline void emit_header_b(Writer& w) {
   w.put('t');
   w.put('h');
   w.put(0);  // 'numpy'
@@ -143,45 +152,90 @@ inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, in
   w.put('b');     // dtype state
   w.put(0x89);    // is_fortran = False
   w.put(']');
-  for (int64_t i = 0; i < count; ++i) {
-    if (i % 1000 == 0) w.put('(');
-    if (i == 0) {
-      w.str("common.crypto.paillier.paillier");
-      w.str("RawCiphertext");
-      w.put(0x93);
-      w.put(0x94);  // memo 1: the class
-    } else {
-      w.put('h');
-      w.put(1);
-    }
-    w.put(')');
-    w.put(0x81);  // NEWOBJ
-    w.put('}');
-    w.put('(');
-    if (i == 0) {
-      w.str("value");
-      w.put(0x94);  // memo 2
-    } else {
-      w.put('h');
-      w.put(2);
-    }
-    put_long(w, ct + (size_t)i * n2w, n2w);
-    if (i == 0) {
-      w.str("exp");
-      w.put(0x94);  // memo 3
-    } else {
-      w.put('h');
-      w.put(3);
-    }
-    w.binint(exps[i]);
-    w.put('u');
-    w.put('b');
-    if (i % 1000 == 999 || i == count - 1) w.put('e');
+}
+
+inline void emit_header(Writer& w, const int64_t* shape, int ndim) {
+  emit_header_a(w);
+  for (int d = 0; d < ndim; ++d) w.binint64(shape[d]);  // the shape tuple's entries
+  emit_header_b(w);
+}
+
+// element i of count: RawCiphertext as NEWOBJ + BUILD({'value': v, 'exp': e});
+// APPENDS batches of 1000 (what CPython emits for a list)
+inline void emit_elem(Writer& w, const uint32_t* row, int n2w, int32_t e, int64_t i, int64_t count) {
+  if (i % 1000 == 0) w.put('(');
+  if (i == 0) {
+    w.str("common.crypto.paillier.paillier");
+    w.str("RawCiphertext");
+    w.put(0x93);
+    w.put(0x94);  // memo 1: the class
+  } else {
+    w.put('h');
+    w.put(1);
   }
+  w.put(')');
+  w.put(0x81);  // NEWOBJ
+  w.put('}');
+  w.put('(');
+  if (i == 0) {
+    w.str("value");
+    w.put(0x94);  // memo 2
+  } else {
+    w.put('h');
+    w.put(2);
+  }
+  put_long(w, row, n2w);
+  if (i == 0) {
+    w.str("exp");
+    w.put(0x94);  // memo 3
+  } else {
+    w.put('h');
+    w.put(3);
+  }
+  w.binint(e);
+  w.put('u');
+  w.put('b');
+  if (i % 1000 == 999 || i == count - 1) w.put('e');
+}
+
+inline void emit_footer(Writer& w) {
   w.put('t');  // state tuple
   w.put('b');  // ndarray.__setstate__
   w.put('.');
-  return w.n;
+}
+
+// Returns the byte count; writes only when out != nullptr and it fits in cap.
+// Elements are sized, prefix-summed and written by `threads` host threads
+// over contiguous element ranges (the bytes do not depend on the split).
+inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                      uint8_t* out, int64_t cap, int threads = 1) {
+  Writer hw{nullptr, 0};
+  emit_header(hw, shape, ndim);
+  const int64_t head = hw.n;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, count / 4096));
+  std::vector<int64_t> part(T + 1, 0);  // element range bounds
+  for (int t = 0; t <= T; ++t) part[t] = count * t / T;
+  std::vector<int64_t> bytes(T, 0);
+  auto sizer = [&](int t) {
+    Writer w{nullptr, 0};
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) emit_elem(w, ct + (size_t)i * n2w, n2w, exps[i], i, count);
+    bytes[t] = w.n;
+  };
+  run_parallel(T, sizer);
+  std::vector<int64_t> off(T + 1, head);
+  for (int t = 0; t < T; ++t) off[t + 1] = off[t] + bytes[t];
+  const int64_t total = off[T] + 3;
+  if (!out || total > cap) return total;
+  Writer h{out, cap};
+  emit_header(h, shape, ndim);
+  auto writer = [&](int t) {
+    Writer w{out + off[t], bytes[t]};
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) emit_elem(w, ct + (size_t)i * n2w, n2w, exps[i], i, count);
+  };
+  run_parallel(T, writer);
+  Writer f{out + off[T], 3};
+  emit_footer(f);
+  return total;
 }
 
 // ------------------------------------------------------------------ decoder
@@ -444,10 +498,137 @@ inline int64_t int_value(const Machine& m, int32_t v) {
   return x.neg ? -(int64_t)u : (int64_t)u;
 }
 
+
+// Bytes of a header part / the first element's class+key strings, built once.
+template <class F>
+std::string emitted(F&& f) {
+  Writer c{nullptr, 0};
+  f(c);
+  std::string s((size_t)c.n, '\0');
+  Writer w{(uint8_t*)&s[0], c.n};
+  f(w);
+  return s;
+}
+
+// Fast path for the exact byte layout `encode` writes (what our peers send):
+// one linear scan, a memcpy per value, no pickle machine. Returns -1 at the
+// first deviation from that layout; decode() then runs the general machine,
+// which accepts (or rejects) every other form of the same object graph.
+inline int64_t decode_own(const uint8_t* p, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
+                          int64_t* shape, int* ndim) {
+  static const std::string A = emitted([](Writer& w) { emit_header_a(w); });
+  static const std::string B = emitted([](Writer& w) { emit_header_b(w); });
+  static const std::string CLS = emitted([](Writer& w) {
+    w.str("common.crypto.paillier.paillier");
+    w.str("RawCiphertext");
+    w.put(0x93);
+    w.put(0x94);
+  });
+  static const std::string VAL = emitted([](Writer& w) { w.str("value"); w.put(0x94); });
+  static const std::string EXP = emitted([](Writer& w) { w.str("exp"); w.put(0x94); });
+  int64_t pos = 0;
+  auto lit = [&](const std::string& s) {
+    if (len - pos < (int64_t)s.size() || memcmp(p + pos, s.data(), s.size()) != 0) return false;
+    pos += (int64_t)s.size();
+    return true;
+  };
+  auto byte = [&](uint8_t b) {
+    if (pos < len && p[pos] == b) {
+      ++pos;
+      return true;
+    }
+    return false;
+  };
+  auto le = [&](int k, uint64_t* v) {
+    if (len - pos < k) return false;
+    uint64_t x = 0;
+    for (int i = 0; i < k; ++i) x |= (uint64_t)p[pos + i] << (8 * i);
+    pos += k;
+    *v = x;
+    return true;
+  };
+  if (!lit(A)) return -1;
+  int nd = 0;
+  while (pos < len && p[pos] != 't') {
+    if (nd >= 8) return -1;
+    uint64_t v;
+    uint8_t op = p[pos++];
+    if (op == 'K') {
+      if (!le(1, &v)) return -1;
+    } else if (op == 'J') {
+      if (!le(4, &v)) return -1;
+      v = (uint64_t)(int64_t)(int32_t)(uint32_t)v;
+    } else if (op == 0x8a) {
+      uint64_t k;
+      if (!le(1, &k) || k != 8 || !le(8, &v)) return -1;
+    } else {
+      return -1;
+    }
+    shape[nd++] = (int64_t)v;
+  }
+  if (!lit(B)) return -1;
+  int64_t i = 0;
+  const int64_t wbytes = 4 * (int64_t)n2w;
+  while (true) {
+    if (i % 1000 == 0) {
+      if (pos < len && p[pos] == 't') break;  // end of the list (no element opens a block here)
+      if (!byte('(')) return -1;
+    }
+    if (i == 0 ? !lit(CLS) : !(byte('h') && byte(1))) return -1;
+    if (!(byte(')') && byte(0x81) && byte('}') && byte('('))) return -1;
+    if (i == 0 ? !lit(VAL) : !(byte('h') && byte(2))) return -1;
+    uint64_t nb;
+    if (byte(0x8a)) {
+      if (!le(1, &nb)) return -1;
+    } else if (byte(0x8b)) {
+      if (!le(4, &nb)) return -1;
+    } else {
+      return -1;
+    }
+    if ((int64_t)nb > len - pos) return -1;
+    const uint8_t* val = p + pos;
+    pos += (int64_t)nb;
+    int64_t used = (int64_t)nb;
+    if (used > 0 && (val[used - 1] & 0x80)) return -1;  // negative: not a ciphertext
+    while (used > 0 && val[used - 1] == 0) --used;
+    if (used > wbytes) return -1;
+    if (i == 0 ? !lit(EXP) : !(byte('h') && byte(3))) return -1;
+    int64_t e;
+    uint64_t v;
+    if (byte('K')) {
+      if (!le(1, &v)) return -1;
+      e = (int64_t)v;
+    } else if (byte('J')) {
+      if (!le(4, &v)) return -1;
+      e = (int64_t)(int32_t)(uint32_t)v;
+    } else {
+      return -1;
+    }
+    if (!(byte('u') && byte('b'))) return -1;
+    if (i < cap_count) {
+      uint8_t* row = (uint8_t*)(ct + (size_t)i * n2w);
+      memcpy(row, val, (size_t)used);
+      memset(row + used, 0, (size_t)(wbytes - used));
+      exps[i] = (int32_t)e;
+    }
+    ++i;
+    const bool closes = pos < len && p[pos] == 'e';
+    if (closes) ++pos;
+    if ((i % 1000 == 0) != closes) {  // a block of 1000 closes exactly at its end, or the list ends
+      if (!closes || !(pos < len && p[pos] == 't')) return -1;
+      break;
+    }
+    if (closes && i % 1000 != 0) break;
+  }
+  if (!(byte('t') && byte('b') && byte('.')) || pos != len) return -1;
+  *ndim = nd;
+  return i;
+}
+
 // Decodes into ct [count][n2w], exps [count]; shape/ndim of the array.
 // Returns the element count; throws on any deviation from the format.
-inline int64_t decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
-                      int64_t* shape, int* ndim) {
+inline int64_t decode_general(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps,
+                              int64_t cap_count, int64_t* shape, int* ndim) {
   Machine m(data, len);
   int32_t top = m.run();
   const Val& arr = m.arena[top];
@@ -490,6 +671,13 @@ inline int64_t decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, i
     exps[i] = (int32_t)e;
   }
   return count;
+}
+
+inline int64_t decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
+                      int64_t* shape, int* ndim) {
+  const int64_t own = decode_own(data, len, n2w, ct, exps, cap_count, shape, ndim);
+  if (own >= 0) return own;
+  return decode_general(data, len, n2w, ct, exps, cap_count, shape, ndim);
 }
 
 }  // namespace wire

@@ -13,20 +13,15 @@
 #include <vector>
 
 #include "../../include/xhe.h"
+#include "abi_common.hpp"
 #include "hostbn.hpp"
-#include "wire.hpp"
 #include "xhe_kernels.hpp"
 
 using namespace xhe;
 
 namespace {
 
-thread_local std::string g_err;
-
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+int fail(int code, const std::string& msg) { return xhe_fail(code, msg); }
 
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
@@ -83,6 +78,16 @@ struct Shape8192 {
   using MN2X = Mont<640, 26, 16>;
 };
 
+// XHE_ONLY_2048: a development build with the 2048-bit shapes only (a
+// fraction of the compile time, for kernel A/B runs through $XHE_LIB); the
+// shipped library has every key size.
+#ifdef XHE_ONLY_2048
+constexpr bool key_bits_supported(int K) { return K == 2048; }
+template <class F>
+decltype(auto) with_shape(int, F&& f) {
+  return f(Shape2048{});
+}
+#else
 constexpr bool key_bits_supported(int K) { return K == 2048 || K == 3072 || K == 4096 || K == 8192; }
 
 // Calls f(ShapeK{}) for the key size K (checked at xhe_key_create).
@@ -93,6 +98,7 @@ decltype(auto) with_shape(int K, F&& f) {
   if (K == 4096) return f(Shape4096{});
   return f(Shape8192{});
 }
+#endif
 
 struct ModSpec {
   int S, W;
@@ -1451,34 +1457,6 @@ int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases,
   });
 }
 
-int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
-                    uint8_t* out, int64_t cap, int64_t* out_len) {
-  return guarded([&]() -> int {
-    if (!out_len || count < 0 || n2w <= 0 || ndim < 0 || ndim > 8 || (count > 0 && (!ct || !exps)) ||
-        (ndim > 0 && !shape))
-      return fail(XHE_EINVAL, "xhe_wire_encode: bad argument");
-    int64_t prod = 1;
-    for (int d = 0; d < ndim; ++d) prod *= shape[d];
-    if (prod != count) return fail(XHE_EINVAL, "xhe_wire_encode: shape does not match count");
-    int64_t need = wire::encode(ct, exps, count, n2w, shape, ndim, out, out ? cap : 0);
-    *out_len = need;
-    if (!out || need > cap) return fail(XHE_EOVERFLOW, "xhe_wire_encode: output buffer too small");
-    return XHE_OK;
-  });
-}
-
-int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
-                    int64_t* count, int64_t* shape, int* ndim) {
-  return guarded([&]() -> int {
-    if (!data || len <= 0 || n2w <= 0 || !count || !shape || !ndim || (cap_count > 0 && (!ct || !exps)))
-      return fail(XHE_EINVAL, "xhe_wire_decode: bad argument");
-    int64_t n = wire::decode(data, len, n2w, ct, exps, cap_count, shape, ndim);
-    *count = n;
-    if (n > cap_count) return fail(XHE_EOVERFLOW, "xhe_wire_decode: output buffers too small");
-    return XHE_OK;
-  });
-}
-
 int xhe_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -1519,7 +1497,5 @@ int xhe_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
   return XHE_OK;
 }
 
-const char* xhe_last_error(void) { return g_err.c_str(); }
-const char* xhe_version(void) { return "xhe 0.1 gfx950"; }
 
 }  // extern "C"

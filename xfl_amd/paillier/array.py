@@ -1,23 +1,36 @@
-"""PaillierArray: the np.ndarray[object] that Paillier.encrypt returns, with
-the element-wise operators, np.sum and np.matmul routed to batched GPU
-kernels instead of one Python call per element.
+"""PaillierArray: the ciphertext array Paillier.encrypt / ciphertext_from /
+the batched operators return - flat buffers underneath, objects on demand.
 
-It is an ndarray subclass, so every reference call site that checks
-`isinstance(x, np.ndarray)`, indexes, reshapes or concatenates keeps working;
-results are bit-identical to the reference's per-element folds (the
-homomorphic sum Prod c_i^(2^(e_i - e_min)) is order-free).
-Anything not recognised falls back to numpy's per-element object loop, which
-calls PaillierCiphertext's own operators (also on the GPU).
+The reference hands out np.ndarray(dtype=object) of PaillierCiphertext, one
+Python object (and one mpz) per element (paillier.py:289-339). Here an array
+is three things: the context, uint32 words [size, n2w] (little-endian
+residues mod n^2, C order over `shape`) and int32 exponents [size] - the
+layout the kernels, the wire codec (include/xhe.h) and RCCL move - and a
+PaillierCiphertext is created only when an element is read. Serialize,
+decrypt, +, -, *, /, np.sum, np.matmul and obfuscate run on the buffers
+without creating Python ints.
+
+Array protocol: shape / ndim / size / len / iteration / indexing / reshape /
+flatten / ravel / transpose / copy / tolist / astype(object), the numpy
+operators and ufuncs, np.sum / np.concatenate / np.stack / np.matmul / np.dot
+through __array_function__, and __array__ for anything else (pandas columns,
+np.asarray, lists of arrays): that materializes the object array the
+reference would have held, so every remaining numpy/pandas path computes
+exactly what the reference computes (per element, through PaillierCiphertext's
+own operators, also on the GPU). Results are bit-identical to the reference's
+per-element folds (the homomorphic sum is order-free).
+
+Differences from an object ndarray: basic slices of a 1-D array share the
+buffers (like numpy views); other indexing returns copies; elements read
+twice are two equal PaillierCiphertext objects, not one; mutate through
+arr[i] = ciphertext, not by mutating an element read earlier.
 """
 import numbers
 
 import numpy as np
 
+from .. import _native as nat
 from . import ops
-
-
-def _is_num(x):
-    return isinstance(x, (int, float)) and not isinstance(x, bool) or isinstance(x, bool)
 
 
 def _ct_type():
@@ -25,179 +38,476 @@ def _ct_type():
     return PaillierCiphertext
 
 
-def _raws(cts):
-    from .paillier import raws_of
-    return raws_of(cts)
-
-
-class PaillierArray(np.ndarray):
-    def __new__(cls, obj):
-        return np.asarray(obj, dtype=object).view(cls)
-
-    def __array_finalize__(self, obj):
-        pass
-
-    # ------------------------------------------------------------ ufuncs
-    def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
-        if method == "__call__" and out is None and not kwargs:
-            try:
-                if ufunc is np.add:
-                    return _add(*inputs)
-                if ufunc is np.subtract:
-                    return _sub(*inputs)
-                if ufunc is np.multiply:
-                    return _mul(*inputs)
-                if ufunc is np.true_divide:
-                    return _div(*inputs)
-                if ufunc is np.matmul:
-                    return _matmul(*inputs)
-            except _Fallback:
-                pass
-        args = [np.asarray(x).view(np.ndarray) if isinstance(x, PaillierArray) else x for x in inputs]
-        if out is not None:
-            out = tuple(np.asarray(o).view(np.ndarray) if isinstance(o, PaillierArray) else o for o in out)
-            kwargs["out"] = out
-        res = getattr(ufunc, method)(*args, **kwargs)
-        return _wrap(res)
-
-    def sum(self, axis=None, dtype=None, out=None, keepdims=False, **kw):
-        if axis is None and out is None and not keepdims and not kw and dtype is None:
-            flat = np.asarray(self).reshape(-1)
-            CT = _ct_type()
-            if flat.size >= 2 and all(isinstance(c, CT) for c in flat):
-                _check_same_key(list(flat))
-                ctx = flat[0].context
-                r, e = ops.segment_sums(ctx, _raws(list(flat)), [c.exponent for c in flat],
-                                        [0, flat.size])
-                return CT(ctx, r[0], int(e[0]))
-        return _wrap(np.ndarray.sum(np.asarray(self).view(np.ndarray), axis=axis, dtype=dtype, out=out,
-                                    keepdims=keepdims, **kw))
+def _same_key(c1, c2):
+    return c1 is c2 or c1 is None or c2 is None or c1.to_public() == c2.to_public()
 
 
 class _Fallback(Exception):
     pass
 
 
+class PaillierArray:
+    __array_priority__ = 1000
+
+    # ------------------------------------------------------------ construction
+    def __init__(self, obj, context=None):
+        """PaillierArray(ciphertexts): from an object array / nested list of
+        PaillierCiphertext (one key), or another PaillierArray (copy)."""
+        if isinstance(obj, PaillierArray):
+            self._set(obj.context, obj._w.copy(), obj._e.copy(), obj._shape)
+            return
+        arr = np.asarray(obj, dtype=object)
+        flat = arr.reshape(-1)
+        CT = _ct_type()
+        for c in flat:
+            if not isinstance(c, CT):
+                raise TypeError(f"PaillierArray holds PaillierCiphertext elements, got {type(c)}")
+        ctx = context
+        if ctx is None:
+            for c in flat:
+                if c.context is not None:
+                    ctx = c.context
+                    break
+        for c in flat:
+            if not _same_key(c.context, ctx):
+                raise ValueError("Adding two ciphertext with different keys.")
+        from .paillier import raws_of
+        raws = raws_of(list(flat))
+        n2w = _n2w(ctx, raws)
+        w = nat.ints_to_words(raws, n2w) if raws else np.zeros((0, n2w), dtype=np.uint32)
+        e = np.fromiter((c.exponent for c in flat), dtype=np.int32, count=flat.size)
+        self._set(ctx, np.ascontiguousarray(w), e, arr.shape)
+
+    @classmethod
+    def from_buffers(cls, context, words, exps, shape=None):
+        """Wrap flat buffers (no copy when already uint32/int32 C-contiguous)."""
+        self = cls.__new__(cls)
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        exps = np.ascontiguousarray(exps, dtype=np.int32).reshape(-1)
+        if shape is None:
+            shape = (exps.shape[0],)
+        if words.ndim != 2:
+            words = words.reshape(exps.shape[0], -1) if exps.shape[0] else np.zeros((0, 1), dtype=np.uint32)
+        self._set(context, words, exps, tuple(int(s) for s in shape))
+        return self
+
+    def _set(self, ctx, w, e, shape):
+        shape = tuple(shape)
+        if int(np.prod(shape, dtype=np.int64)) != e.shape[0] or w.shape[0] != e.shape[0]:
+            raise ValueError(f"PaillierArray: {w.shape[0]} rows / {e.shape[0]} exponents for shape {shape}")
+        self.context = ctx
+        self._w = w
+        self._e = e
+        self._shape = shape
+
+    # ------------------------------------------------------------ buffers
+    @property
+    def words(self):
+        """uint32 [size, n2w] residues mod n^2 (C order over shape)"""
+        return self._w
+
+    @property
+    def exponents(self):
+        """int32 [size] exponents"""
+        return self._e
+
+    # ------------------------------------------------------------ ndarray-like surface
+    @property
+    def shape(self):
+        return self._shape
+
+    @property
+    def ndim(self):
+        return len(self._shape)
+
+    @property
+    def size(self):
+        return self._e.shape[0]
+
+    @property
+    def dtype(self):
+        return np.dtype(object)
+
+    @property
+    def T(self):
+        return self.transpose()
+
+    def __len__(self):
+        if not self._shape:
+            raise TypeError("len() of unsized object")
+        return self._shape[0]
+
+    def __repr__(self):
+        return f"PaillierArray(shape={self._shape}, key_bits={None if self.context is None else self.context.n.bit_length()})"
+
+    def _elem(self, i, raw=None):
+        CT = _ct_type()
+        if raw is None:
+            raw = int.from_bytes(self._w[i].tobytes(), "little")
+        return CT(self.context, raw, int(self._e[i]))
+
+    def _take(self, flat_idx, shape):
+        flat_idx = np.asarray(flat_idx, dtype=np.int64).reshape(-1)
+        return PaillierArray.from_buffers(self.context, self._w[flat_idx], self._e[flat_idx], shape)
+
+    def _index_map(self):
+        return np.arange(self.size, dtype=np.int64).reshape(self._shape)
+
+    def __getitem__(self, key):
+        if self.ndim == 1:
+            if isinstance(key, (int, np.integer)):
+                i = int(key)
+                if i < -self.size or i >= self.size:
+                    raise IndexError(f"index {i} is out of bounds for axis 0 with size {self.size}")
+                return self._elem(i % self.size)
+            if isinstance(key, slice) and (key.step is None or key.step == 1):
+                lo, hi, _ = key.indices(self.size)
+                hi = max(lo, hi)
+                return PaillierArray.from_buffers(self.context, self._w[lo:hi], self._e[lo:hi], (hi - lo,))
+        if isinstance(key, tuple) and len(key) == self.ndim and all(isinstance(k, (int, np.integer)) for k in key):
+            idx = np.ravel_multi_index(tuple(int(k) % s for k, s in zip(key, self._shape)), self._shape)
+            return self._elem(int(idx))
+        sel = self._index_map()[key]
+        if np.ndim(sel) == 0:
+            return self._elem(int(sel))
+        return self._take(sel, sel.shape)
+
+    def __setitem__(self, key, value):
+        sel = np.asarray(self._index_map()[key], dtype=np.int64)
+        src = _as_cipher(value)
+        if src is None:
+            raise TypeError(f"can only assign PaillierCiphertext values, got {type(value)}")
+        if not _same_key(src.context, self.context):
+            raise ValueError("Adding two ciphertext with different keys.")
+        src = src._aligned_words(self._w.shape[1])
+        ib = np.broadcast_to(src._index_map(), sel.shape).reshape(-1)
+        self._w[sel.reshape(-1)] = src._w[ib]
+        self._e[sel.reshape(-1)] = src._e[ib]
+
+    def __iter__(self):
+        if self.ndim == 0:
+            raise TypeError("iteration over a 0-d array")
+        if self.ndim == 1:
+            raws = nat.words_to_ints(self._w) if self.size else []
+            for i, r in enumerate(raws):
+                yield self._elem(i, r)
+        else:
+            for i in range(self._shape[0]):
+                yield self[i]
+
+    def reshape(self, *shape, order="C"):
+        if order not in ("C", "A"):
+            raise _unsupported("reshape(order='F')")
+        if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
+            shape = tuple(shape[0])
+        new = np.empty(self._shape, dtype=np.bool_).reshape(shape).shape  # numpy's -1 / size rules
+        return PaillierArray.from_buffers(self.context, self._w, self._e, new)
+
+    def flatten(self, order="C"):
+        return self.reshape(-1).copy() if order in ("C", "A") else self.transpose().reshape(-1)
+
+    def ravel(self, order="C"):
+        return self.reshape(-1) if order in ("C", "A") else self.transpose().reshape(-1)
+
+    def transpose(self, *axes):
+        if self.ndim < 2:
+            return self
+        perm = self._index_map().transpose(*axes) if axes else self._index_map().T
+        return self._take(perm, perm.shape)
+
+    def squeeze(self, axis=None):
+        return self.reshape(np.empty(self._shape, dtype=np.bool_).squeeze(axis).shape)
+
+    def copy(self, order="C"):
+        return PaillierArray.from_buffers(self.context, self._w.copy(), self._e.copy(), self._shape)
+
+    def tolist(self):
+        return self._objects().tolist()
+
+    def astype(self, dtype, copy=True):
+        if np.dtype(dtype) == np.dtype(object):
+            return self.copy() if copy else self
+        return self._objects().astype(dtype)
+
+    def _objects(self):
+        """The reference's representation: np.ndarray[object] of PaillierCiphertext."""
+        out = np.empty(self.size, dtype=object)
+        if self.size:
+            for i, r in enumerate(nat.words_to_ints(self._w)):
+                out[i] = self._elem(i, r)
+        return out.reshape(self._shape)
+
+    def __array__(self, dtype=None, copy=None):
+        arr = self._objects()
+        return arr if dtype is None or np.dtype(dtype) == np.dtype(object) else arr.astype(dtype)
+
+    def __reduce__(self):
+        return (PaillierArray.from_buffers, (self.context, self._w, self._e, self._shape))
+
+    def _aligned_words(self, n2w):
+        """self with n2w-word rows (arrays decoded without a context keep the
+        wire's width)."""
+        if self._w.shape[1] == n2w:
+            return self
+        if self._w.shape[1] > n2w:
+            if self._w[:, n2w:].any():
+                raise ValueError("ciphertext wider than the key's n^2")
+            w = np.ascontiguousarray(self._w[:, :n2w])
+        else:
+            w = np.zeros((self.size, n2w), dtype=np.uint32)
+            w[:, :self._w.shape[1]] = self._w
+        return PaillierArray.from_buffers(self.context, w, self._e, self._shape)
+
+    # ------------------------------------------------------------ reductions
+    def sum(self, axis=None, dtype=None, out=None, keepdims=False, initial=None, where=None):
+        if out is not None or dtype not in (None, object) or where is not None or initial is not None:
+            return _obj_call(np.sum, (self,), dict(axis=axis, dtype=dtype, out=out, keepdims=keepdims,
+                                                   initial=initial, where=where))
+        return _sum(self, axis, keepdims)
+
+    # ------------------------------------------------------------ operators
+    def __add__(self, other):
+        return _dispatch(_add, self, other, np.add)
+
+    def __radd__(self, other):
+        return _dispatch(_add, other, self, np.add)
+
+    def __sub__(self, other):
+        return _dispatch(_sub, self, other, np.subtract)
+
+    def __rsub__(self, other):
+        return _dispatch(_sub, other, self, np.subtract)
+
+    def __mul__(self, other):
+        return _dispatch(_mul, self, other, np.multiply)
+
+    def __rmul__(self, other):
+        return _dispatch(_mul, other, self, np.multiply)
+
+    def __truediv__(self, other):
+        return _dispatch(_div, self, other, np.true_divide)
+
+    def __rtruediv__(self, other):
+        return _dispatch(_div, other, self, np.true_divide)
+
+    def __matmul__(self, other):
+        return _dispatch(_matmul, self, other, np.matmul)
+
+    def __rmatmul__(self, other):
+        return _dispatch(_matmul, other, self, np.matmul)
+
+    def __neg__(self):
+        return _mul(self, -1)
+
+    def __pos__(self):
+        return self
+
+    # ------------------------------------------------------------ numpy protocols
+    def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
+        if method == "__call__" and out is None and not kwargs:
+            fn = _UFUNCS.get(ufunc)
+            if fn is not None:
+                try:
+                    return fn(*inputs)
+                except _Fallback:
+                    pass
+        if out is not None:
+            kwargs["out"] = tuple(_plain(o) for o in out)
+        return _wrap(getattr(ufunc, method)(*[_plain(x) for x in inputs], **kwargs))
+
+    def __array_function__(self, func, types, args, kwargs):
+        fn = _FUNCS.get(func)
+        if fn is not None:
+            try:
+                return fn(*args, **kwargs)
+            except _Fallback:
+                pass
+        return _obj_call(func, args, kwargs)
+
+
+def _unsupported(what):
+    return NotImplementedError(f"PaillierArray.{what} is not supported")
+
+
+def _n2w(ctx, raws=()):
+    if ctx is not None:
+        return ops.n2w_of(ctx)
+    bits = max((int(r).bit_length() for r in raws), default=1)
+    for k in (2048, 3072, 4096, 8192):
+        if bits <= 2 * k:
+            return 2 * k // 32
+    return (bits + 31) // 32
+
+
+def _plain(x):
+    """PaillierArray -> the reference's object array (recursively in lists)."""
+    if isinstance(x, PaillierArray):
+        return x._objects()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_plain(v) for v in x)
+    return x
+
+
+def _obj_call(func, args, kwargs):
+    return _wrap(func(*[_plain(a) for a in args], **{k: _plain(v) for k, v in kwargs.items()}))
+
+
 def _wrap(res):
-    if isinstance(res, np.ndarray) and res.dtype == object and not isinstance(res, PaillierArray):
-        return res.view(PaillierArray)
+    """Object arrays of ciphertexts of one key come back as PaillierArray;
+    anything else is returned as numpy made it."""
+    if isinstance(res, np.ndarray) and res.dtype == object and res.size:
+        CT = _ct_type()
+        flat = res.reshape(-1)
+        if all(isinstance(c, CT) for c in flat):
+            ctx = flat[0].context
+            if all(_same_key(c.context, ctx) for c in flat):
+                return PaillierArray(res)
     return res
 
 
-def _obj(x):
-    return np.asarray(x, dtype=object) if not isinstance(x, np.ndarray) or x.dtype == object else x.astype(object)
+def _as_cipher(x):
+    """x as a PaillierArray when it is ciphertext-only, else None."""
+    if isinstance(x, PaillierArray):
+        return x
+    CT = _ct_type()
+    if isinstance(x, CT):
+        return PaillierArray(np.array(x, dtype=object).reshape(()))
+    if isinstance(x, (list, tuple)) or (isinstance(x, np.ndarray) and x.dtype == object):
+        arr = np.asarray(x, dtype=object) if not (isinstance(x, np.ndarray)) else x
+        if arr.size and all(isinstance(c, CT) for c in arr.reshape(-1)):
+            return PaillierArray(arr)
+    return None
 
 
-def _check_same_key(cts):
-    seen = {}
-    first = cts[0].context
-    for c in cts:
-        k = id(c.context)
-        if k in seen:
-            continue
-        seen[k] = True
-        if c.context is not first and c.context.to_public() != first.to_public():
-            raise ValueError("Adding two ciphertext with different keys.")
+def _as_plain(x):
+    """x as a numeric array of plaintext scalars, or None. Python numbers and
+    numeric ndarrays (numpy casts their elements to Python scalars in the
+    reference's object loops, so float32 elements are exact floats there)."""
+    if isinstance(x, PaillierArray) or isinstance(x, _ct_type()):
+        return None
+    if isinstance(x, bool) or isinstance(x, (int, float)) and not isinstance(x, np.generic):
+        return np.asarray(x, dtype=object if isinstance(x, int) and abs(x) >= 2 ** 63 else None)
+    if isinstance(x, np.generic) and x.dtype.kind in "biuf":
+        return np.asarray(x)
+    if isinstance(x, np.ndarray):
+        if x.dtype.kind in "biuf":
+            return x
+        if x.dtype == object and x.size and all(isinstance(v, (int, float)) for v in x.reshape(-1)):
+            return x
+    if isinstance(x, (list, tuple)):
+        try:
+            a = np.asarray(x)
+        except (ValueError, TypeError):
+            return None
+        return _as_plain(a) if a.dtype.kind in "biuf" or a.dtype == object else None
+    return None
+
+
+def _dispatch(fn, a, b, ufunc):
+    try:
+        return fn(a, b)
+    except _Fallback:
+        return _wrap(ufunc(_plain(a), _plain(b)))
+
+
+def _bcast(a, b):
+    """broadcast flat index maps of two operands -> (ia, ib, shape)"""
+    sa = a.shape if hasattr(a, "shape") else ()
+    sb = b.shape if hasattr(b, "shape") else ()
+    shape = np.broadcast_shapes(sa, sb)
+    ia = np.broadcast_to(np.arange(int(np.prod(sa, dtype=np.int64)), dtype=np.int64).reshape(sa), shape).reshape(-1)
+    ib = np.broadcast_to(np.arange(int(np.prod(sb, dtype=np.int64)), dtype=np.int64).reshape(sb), shape).reshape(-1)
+    return ia, ib, shape
+
+
+def _rows(x, idx):
+    """rows of x at idx, without a copy when idx is the identity"""
+    if idx.shape[0] == x.size and (x.size == 0 or (idx[0] == 0 and np.all(np.diff(idx) == 1))):
+        return x._w, x._e
+    return x._w[idx], x._e[idx]
+
+
+def _ctx_of(*xs):
+    ctx = None
+    for x in xs:
+        if x.context is not None:
+            if ctx is not None and not _same_key(ctx, x.context):
+                raise ValueError("Adding two ciphertext with different keys.")
+            ctx = ctx or x.context
+    if ctx is None:
+        raise ValueError("ciphertext array without a context: pass one to Paillier.ciphertext_from")
+    return ctx
+
+
+def _result(ctx, w, e, shape):
+    return PaillierArray.from_buffers(ctx, w, e, shape)
+
+
+# ------------------------------------------------------------ element-wise ops
+def _encrypt_plain(ctx, vals):
+    """Paillier.encrypt(scalar, precision=None, obfuscation=False) of every
+    element (the scalar operand of PaillierCiphertext.__add__, paillier.py:96-98)."""
+    from .paillier import Paillier
+    arr = Paillier.encrypt(ctx, np.asarray(vals).reshape(-1) if np.ndim(vals) else np.asarray(vals).reshape(1),
+                           precision=None, max_exponent=None, obfuscation=False)
+    return arr
 
 
 def _add(a, b):
-    """element-wise a + b with the reference's semantics (paillier.py:88-126)."""
-    CT = _ct_type()
-    A, B = np.broadcast_arrays(_obj(a), _obj(b))
-    shape = A.shape
-    A, B = A.reshape(-1), B.reshape(-1)
-    n = A.size
-    out = np.empty(n, dtype=object)
-    pairs, scal = [], []
-    for i in range(n):
-        x, y = A[i], B[i]
-        xc, yc = isinstance(x, CT), isinstance(y, CT)
-        if xc and yc:
-            pairs.append((i, x, y))
-        elif xc or yc:
-            c, s = (x, y) if xc else (y, x)
-            if not isinstance(s, (int, float)):
-                raise TypeError(f"Adding data of type {type(s)} not supported.")
-            scal.append((i, c, s))
-        else:
-            raise _Fallback()
-    if pairs:
-        _check_same_key([p[1] for p in pairs] + [p[2] for p in pairs])
-        ctx = pairs[0][1].context
-        r, e = ops.add(ctx, _raws([p[1] for p in pairs]), [p[1].exponent for p in pairs],
-                       _raws([p[2] for p in pairs]), [p[2].exponent for p in pairs])
-        for (i, x, _), rv, ev in zip(pairs, r, e):
-            out[i] = CT(x.context, rv, int(ev))
-    if scal:
-        from .paillier import Paillier
-        ctx = scal[0][1].context
-        enc = Paillier.encrypt(ctx, np.array([s for _, _, s in scal], dtype=object), precision=None,
-                               max_exponent=None, obfuscation=False)
-        r, e = ops.add(ctx, _raws([c for _, c, _ in scal]), [c.exponent for _, c, _ in scal],
-                       [c.raw_ciphertext for c in enc], [c.exponent for c in enc])
-        for (i, c, _), rv, ev in zip(scal, r, e):
-            out[i] = CT(c.context, rv, int(ev))
-    return out.reshape(shape).view(PaillierArray)
+    """a + b with the reference's semantics (paillier.py:88-126)."""
+    ca, cb = _as_cipher(a), _as_cipher(b)
+    if ca is not None and cb is not None:
+        ctx = _ctx_of(ca, cb)
+        n2w = ops.n2w_of(ctx)
+        ca, cb = ca._aligned_words(n2w), cb._aligned_words(n2w)
+        ia, ib, shape = _bcast(ca, cb)
+        wa, ea = _rows(ca, ia)
+        wb, eb = _rows(cb, ib)
+        w, e = ops.add_words(ctx, wa, ea, wb, eb)
+        return _result(ctx, w, e, shape)
+    if ca is None and cb is not None:
+        a, b, ca, cb = b, a, cb, ca
+    if ca is None:
+        raise _Fallback()
+    p = _as_plain(b)
+    if p is None:
+        if isinstance(b, (str, bytes)) or not hasattr(b, "__len__"):
+            raise TypeError(f"Adding data of type {type(b)} not supported.")
+        raise _Fallback()
+    ctx = _ctx_of(ca)
+    ca = ca._aligned_words(ops.n2w_of(ctx))
+    ia, ib, shape = _bcast(ca, p)
+    enc = _encrypt_plain(ctx, np.asarray(p).reshape(-1)[ib] if p.ndim else np.repeat(np.asarray(p).reshape(1), ib.size))
+    wa, ea = _rows(ca, ia)
+    w, e = ops.add_words(ctx, wa, ea, enc._w, enc._e)
+    return _result(ctx, w, e, shape)
 
 
-def _mul(a, b):
-    """element-wise ciphertext * scalar (paillier.py:134-148)."""
-    from .encoder import PaillierEncoder
-    CT = _ct_type()
-    A, B = np.broadcast_arrays(_obj(a), _obj(b))
-    shape = A.shape
-    A, B = A.reshape(-1), B.reshape(-1)
-    n = A.size
-    out = np.empty(n, dtype=object)
-    items = []
-    for i in range(n):
-        x, y = A[i], B[i]
-        xc, yc = isinstance(x, CT), isinstance(y, CT)
-        if xc and yc:
-            raise TypeError("Cannot multiply one ciphertext with another ciphertext, try multiply a scalar.")
-        if not (xc or yc):
-            raise _Fallback()
-        c, s = (x, y) if xc else (y, x)
-        items.append((i, c, s))
-    if items:
-        ctx = items[0][1].context
-        ks, es = [], []
-        for _, c, s in items:
-            e = PaillierEncoder.cal_exponent(s, precision=None)
-            ks.append(int(PaillierEncoder.encode_single(c.context, s, e)))
-            es.append(int(e))
-        r = ops.raw_mul(ctx, _raws([c for _, c, _ in items]), ks)
-        for (i, c, _), rv, ev in zip(items, r, es):
-            out[i] = CT(c.context, rv, ev + c.exponent)
-    return out.reshape(shape).view(PaillierArray)
-
-
-def _neg_each(x):
-    return _mul(x, -1) if _has_ct(x) else np.negative(_obj(x))
-
-
-def _has_ct(x):
-    CT = _ct_type()
-    return any(isinstance(v, CT) for v in np.asarray(x, dtype=object).reshape(-1))
+def _neg_plain(p):
+    """other * (-1) of a plaintext operand (paillier.py:128-132), elementwise"""
+    if p.dtype == object:
+        return np.vectorize(lambda v: v * (-1), otypes=[object])(p)
+    if p.dtype.kind == "u" or p.dtype == np.bool_:
+        return (-p.astype(object)) if p.dtype.kind == "u" else -(p.astype(np.int64))
+    return -p
 
 
 def _sub(a, b):
-    # a - b = a + b*(-1)  (paillier.py:128-132: scalar - ct = (-1)*ct + scalar)
-    if _has_ct(b):
-        return _add(a, _mul(b, -1))
-    return _add(a, np.negative(_obj(b)))
-
-
-def _div(a, b):
-    if _has_ct(b):
+    """a - b = a + b * (-1); scalar - ct = (-1) * ct + scalar (paillier.py:128-132)."""
+    cb = _as_cipher(b)
+    if cb is not None:
+        return _add(a, _mul(cb, -1))
+    if _as_cipher(a) is None:
         raise _Fallback()
-    B = _obj(b)
-    return _mul(a, np.vectorize(lambda s: 1 / s, otypes=[object])(B))
+    p = _as_plain(b)
+    if p is None:
+        raise _Fallback()
+    return _add(a, _neg_plain(p))
 
 
 def _encode_scalars_vec(X):
     """Vectorised PaillierEncoder.cal_exponent(precision=None) + encode_single
-    (encoder.py:29-54) of a plain numeric matrix, as (|k|, k negative, e):
+    (encoder.py:29-54) of a plain numeric array, as (|k|, k negative, e):
     floats give e = frexp exponent - 53 and |k| = |mantissa| * 2^53 (exact),
     ints e = 0 and |k| = |x|; a negative value encodes to n - |k|, which is
     >= min_value_for_negative for every |k| < 2^63 (the _raw_mul negative
@@ -212,7 +522,7 @@ def _encode_scalars_vec(X):
         mant, expo = np.frexp(x)
         kabs = (np.abs(mant) * 2.0 ** 53).astype(np.int64)
         return kabs, x < 0, expo.astype(np.int64) - 53
-    if X.dtype.kind in "iu" and X.dtype.itemsize <= 8:
+    if X.dtype.kind in "iub" and X.dtype.itemsize <= 8:
         if X.dtype.kind == "u" and X.size and int(X.max()) >= 2 ** 63:
             return None
         x = X.astype(np.int64)
@@ -222,58 +532,229 @@ def _encode_scalars_vec(X):
     return None
 
 
-def _matmul(a, b):
-    """enc[B] @ X[B, D] (logistic_regression/trainer.py:166): per output j,
-    Prod_i base_i^(k'_ij * 2^(d_ij)) with base_i = c_i or c_i^-1 (negative
-    scalars), d_ij aligning e_i + e_kij to the column minimum; = the
-    reference's object-dtype dot product bit for bit."""
+def _encode_scalars(ctx, P):
+    """(|k| words, negative flags, exponents) of every scalar of P (flat)."""
     from .encoder import PaillierEncoder
-    CT = _ct_type()
-    A = np.asarray(a, dtype=object)
-    X = np.asarray(b)
-    if A.ndim != 1 or X.ndim != 2 or X.dtype == object or A.shape[0] != X.shape[0] or A.shape[0] == 0:
-        raise _Fallback()
-    if not all(isinstance(c, CT) for c in A):
-        raise _Fallback()
-    _check_same_key(list(A))
-    ctx = A[0].context
-    Bn, D = X.shape
-    cexp = np.array([c.exponent for c in A], dtype=np.int64)
-    vec = _encode_scalars_vec(X)
+    vec = _encode_scalars_vec(P) if P.dtype != object else None
     if vec is not None:
-        kabs, neg_a, e_a = vec
-        ks = kabs.tolist()
-        neg = neg_a.tolist()
-        ex = cexp[:, None] + e_a
+        kabs, neg, e = vec
+        return kabs.reshape(-1), neg.reshape(-1), e.reshape(-1)
+    thr = ctx.min_value_for_negative
+    ks, neg, es = [], [], []
+    for s in P.reshape(-1):
+        s = s.item() if isinstance(s, np.generic) else s
+        e = PaillierEncoder.cal_exponent(s, precision=None)
+        k = int(PaillierEncoder.encode_single(ctx, s, e))
+        if k >= thr:
+            ks.append(ctx.n - k)
+            neg.append(True)
+        else:
+            ks.append(k)
+            neg.append(False)
+        es.append(int(e))
+    kbits = max(1, max(k.bit_length() for k in ks))
+    return nat.ints_to_words(ks, (kbits + 31) // 32), np.array(neg, dtype=bool), np.array(es, dtype=np.int64)
+
+
+def _mul(a, b):
+    """ciphertext * scalar element-wise (paillier.py:134-187)."""
+    ca, cb = _as_cipher(a), _as_cipher(b)
+    if ca is not None and cb is not None:
+        raise TypeError("Cannot multiply one ciphertext with another ciphertext, try multiply a scalar.")
+    if ca is None and cb is not None:
+        a, b, ca = b, a, cb
+    if ca is None:
+        raise _Fallback()
+    p = _as_plain(b)
+    if p is None:
+        if isinstance(b, (str, bytes)) or not hasattr(b, "__len__"):
+            raise TypeError(f"Precision type {type(None)} not supported.")
+        raise _Fallback()
+    ctx = _ctx_of(ca)
+    ca = ca._aligned_words(ops.n2w_of(ctx))
+    ia, ib, shape = _bcast(ca, p)
+    P = np.asarray(p).reshape(-1)[ib] if np.ndim(p) else np.repeat(np.asarray(p).reshape(1), ib.size)
+    kabs, neg, ek = _encode_scalars(ctx, P)
+    wa, ea = _rows(ca, ia)
+    w = ops.raw_mul_words(ctx, wa, kabs, neg)
+    e = (ea.astype(np.int64) + ek).astype(np.int32)
+    return _result(ctx, w, e, shape)
+
+
+def _div(a, b):
+    """ct / s = ct * (1 / s) (paillier.py:150-151), 1/s in float64 per element."""
+    if _as_cipher(b) is not None or _as_cipher(a) is None:
+        raise _Fallback()
+    p = _as_plain(b)
+    if p is None:
+        raise _Fallback()
+    if p.dtype == object:
+        inv = np.vectorize(lambda s: 1 / s, otypes=[object])(p)
     else:
-        thr = ctx.min_value_for_negative
-        ks = [[0] * D for _ in range(Bn)]
-        neg = [[False] * D for _ in range(Bn)]
-        ex = np.zeros((Bn, D), dtype=np.int64)
-        for i in range(Bn):
-            for j in range(D):
-                s = X[i, j].item()
-                e = PaillierEncoder.cal_exponent(s, precision=None)
-                k = int(PaillierEncoder.encode_single(ctx, s, e))
-                if k >= thr:
-                    ks[i][j], neg[i][j] = ctx.n - k, True
-                else:
-                    ks[i][j] = k
-                ex[i, j] = cexp[i] + e
+        inv = 1.0 / np.asarray(p, dtype=np.float64)
+    return _mul(a, inv)
+
+
+# ------------------------------------------------------------ reductions
+def _sum(x, axis=None, keepdims=False):
+    """np.sum over ciphertexts: per output element the order-free product
+    prod c_i^(2^(e_i - e_min)) (paillier.py:79-123 folded)."""
+    ctx = _ctx_of(x)
+    x = x._aligned_words(ops.n2w_of(ctx))
+    if x.ndim == 0:
+        return x._elem(0)
+    if axis is None:
+        axes = tuple(range(x.ndim))
+    else:
+        axes = tuple(sorted(a % x.ndim for a in (axis if isinstance(axis, tuple) else (axis,))))
+    keep = [d for d in range(x.ndim) if d not in axes]
+    perm = x._index_map().transpose(keep + list(axes))
+    out_shape = tuple(x.shape[d] for d in keep)
+    nseg = int(np.prod(out_shape, dtype=np.int64))
+    seglen = x.size // nseg if nseg else 0
+    if seglen == 0:
+        raise _Fallback()  # empty reduction: the reference's object sum gives int 0
+    order = perm.reshape(-1)
+    w, e = _rows(x, order)
+    seg = np.arange(nseg + 1, dtype=np.int64) * seglen
+    rw, re = ops.segment_sums_words(ctx, w, e, seg)
+    if keepdims:
+        out_shape = tuple(1 if d in axes else x.shape[d] for d in range(x.ndim))
+    if not out_shape:
+        return _result(ctx, rw, re, (1,))._elem(0)
+    return _result(ctx, rw, re, out_shape)
+
+
+def _f_sum(a, axis=None, dtype=None, out=None, keepdims=False, initial=None, where=None):
+    c = _as_cipher(a)
+    if c is None or out is not None or dtype not in (None, object) or initial is not None or where is not None:
+        raise _Fallback()
+    return _sum(c, axis, keepdims)
+
+
+def _f_concatenate(arrays, axis=0, out=None, dtype=None, casting="same_kind"):
+    if out is not None or dtype not in (None, object):
+        raise _Fallback()
+    cs = [_as_cipher(a) for a in arrays]
+    if not cs or any(c is None for c in cs):
+        raise _Fallback()
+    ctx = _ctx_of(*cs)
+    n2w = ops.n2w_of(ctx)
+    cs = [c._aligned_words(n2w) for c in cs]
+    if axis is None:
+        cs = [c.reshape(-1) for c in cs]
+        axis = 0
+    idx_parts, off = [], 0
+    for c in cs:
+        idx_parts.append(c._index_map() + off)
+        off += c.size
+    idx = np.concatenate(idx_parts, axis=axis)
+    w = np.concatenate([c._w for c in cs]) if cs else np.zeros((0, n2w), np.uint32)
+    e = np.concatenate([c._e for c in cs])
+    flat = idx.reshape(-1)
+    return _result(ctx, w[flat], e[flat], idx.shape)
+
+
+def _f_stack(arrays, axis=0, out=None, dtype=None, casting="same_kind"):
+    if out is not None or dtype not in (None, object) or axis != 0:
+        raise _Fallback()
+    cs = [_as_cipher(a) for a in arrays]
+    if not cs or any(c is None for c in cs) or len({c.shape for c in cs}) != 1:
+        raise _Fallback()
+    return _f_concatenate([c.reshape((1,) + c.shape) for c in cs], axis=0)
+
+
+def _f_reshape(a, *args, **kw):
+    if isinstance(a, PaillierArray):
+        newshape = kw.pop("newshape", kw.pop("shape", args[0] if args else None))
+        return a.reshape(newshape, order=kw.get("order", "C"))
+    raise _Fallback()
+
+
+def _f_ravel(a, order="C"):
+    if isinstance(a, PaillierArray):
+        return a.ravel(order)
+    raise _Fallback()
+
+
+def _f_shape(a):
+    return a.shape
+
+
+def _f_ndim(a):
+    return a.ndim
+
+
+def _f_size(a, axis=None):
+    return a.size if axis is None else a.shape[axis]
+
+
+def _f_copy(a, order="K", subok=False):
+    return a.copy()
+
+
+def _f_transpose(a, axes=None):
+    return a.transpose(*(axes or ()))
+
+
+# ------------------------------------------------------------ matmul
+def _matmul(a, b):
+    """enc[B] @ X[B, D] (logistic_regression/trainer.py:166) and X[D, B] @
+    enc[B]: per output j the multi-exponentiation prod_i base_i^(k'_ij *
+    2^(d_ij)) with base_i = c_i or c_i^-1 (negative scalars) and d_ij aligning
+    e_i + e_kij to the column minimum = the reference's object-dtype dot
+    product (a fold of __mul__ + __add__) bit for bit."""
+    ca, cb = _as_cipher(a), _as_cipher(b)
+    if ca is not None and cb is not None:
+        raise TypeError("Cannot multiply one ciphertext with another ciphertext, try multiply a scalar.")
+    if ca is not None:
+        X = _as_plain(b)
+        if X is None or ca.ndim != 1 or np.ndim(X) != 2 or X.shape[0] != ca.shape[0] or ca.size == 0:
+            raise _Fallback()
+        return _matvec(ca, X)
+    if cb is not None:
+        X = _as_plain(a)
+        if X is None or cb.ndim != 1 or np.ndim(X) != 2 or X.shape[1] != cb.shape[0] or cb.size == 0:
+            raise _Fallback()
+        return _matvec(cb, np.asarray(X).T)
+    raise _Fallback()
+
+
+def _matvec(A, X):
+    ctx = _ctx_of(A)
+    A = A._aligned_words(ops.n2w_of(ctx))
+    Bn, D = X.shape
+    cexp = A._e.astype(np.int64)
+    kw_, neg, e_k = _encode_scalars(ctx, np.asarray(X))
+    if kw_.ndim == 1:  # int64 |k| from the vectorised encoder
+        kw_ = np.ascontiguousarray(kw_, dtype=np.uint64).view(np.uint32).reshape(-1, 2)
+    ks = nat.words_to_ints(kw_)  # |k_ij|, row-major [B, D]
+    neg = neg.reshape(Bn, D)
+    ex = cexp[:, None] + e_k.reshape(Bn, D)
     emin = ex.min(axis=0)
-    need_inv = [i for i in range(Bn) if any(neg[i])]
-    # bases: the B ciphertexts, then the inverses of those with a negative scalar
-    bases = _raws(list(A))
-    inv_slot = {}
-    if need_inv:
-        r = ops.powmod(ctx, [bases[i] for i in need_inv], [1] * len(need_inv), invert_first=True)
-        for i, v in zip(need_inv, r):
-            inv_slot[i] = len(bases)
-            bases.append(v)
-    idx = [[inv_slot[i] if neg[i][j] else i for i in range(Bn)] for j in range(D)]
-    exps = [[ks[i][j] << int(ex[i, j] - emin[j]) for i in range(Bn)] for j in range(D)]
-    r = ops.multiexp(ctx, bases, idx, exps)
-    out = np.empty(D, dtype=object)
-    for j in range(D):
-        out[j] = CT(ctx, r[j], int(emin[j]))
-    return out.view(PaillierArray)
+    need_inv = np.nonzero(neg.any(axis=1))[0]
+    bases = A._w
+    inv_slot = np.full(Bn, -1, dtype=np.int64)
+    if need_inv.size:
+        one = np.zeros((need_inv.size, 1), dtype=np.uint32)
+        one[:, 0] = 1
+        inv = ops.powmod_words(ctx, A._w[need_inv], one, 1, invert_first=True)
+        inv_slot[need_inv] = Bn + np.arange(need_inv.size)
+        bases = np.concatenate([A._w, inv])
+    rows = np.arange(Bn, dtype=np.int64)
+    idx = np.where(neg, inv_slot[:, None], rows[:, None]).T.astype(np.int32)  # [D, B]
+    shift = (ex - emin[None, :]).T  # [D, B]
+    exps = [ks[i * D + j] << int(shift[j, i]) for j in range(D) for i in range(Bn)]
+    kbits = max(1, max(k.bit_length() for k in exps))
+    kw = (kbits + 31) // 32
+    r = ops.multiexp_words(ctx, bases, idx, nat.ints_to_words(exps, kw), kbits)
+    return _result(ctx, r, emin.astype(np.int32), (D,))
+
+
+_UFUNCS = {np.add: _add, np.subtract: _sub, np.multiply: _mul, np.true_divide: _div, np.matmul: _matmul,
+           np.negative: lambda a: _mul(a, -1)}
+_FUNCS = {np.sum: _f_sum, np.concatenate: _f_concatenate, np.reshape: _f_reshape, np.ravel: _f_ravel,
+          np.shape: _f_shape, np.ndim: _f_ndim, np.size: _f_size, np.copy: _f_copy, np.transpose: _f_transpose,
+          np.matmul: lambda a, b, **kw: _dispatch(_matmul, a, b, np.matmul) if not kw else _obj_call(np.matmul, (a, b), kw),
+          np.dot: lambda a, b, out=None: _dispatch(_matmul, a, b, np.dot) if out is None else _obj_call(np.dot, (a, b), {"out": out}),
+          np.stack: _f_stack}

@@ -6,14 +6,17 @@ device-resident key (constants + fixed-base tables, include/xhe.h
 xhe_key_create) is built lazily on first use and cached per context.
 """
 import math
+import os
 import pickle
 import secrets
+import threading
 import warnings
 from typing import Optional
 
 from .utils import getprimeover, invert
 
 SUPPORTED_DEVICE_BITS = (2048, 3072, 4096, 8192)
+_KEY_LOCK = threading.Lock()
 
 
 def device_key_bits(n):
@@ -180,19 +183,82 @@ class PaillierContext(object):
         return invert(self._l_function(pow(self.__n + 1, x - 1, xsquare), x), x)
 
     # ------------------------------------------------------------ device
+    # Fixed-base table window (DJN private keys, include/xhe.h xhe_key_create):
+    # a wider window means fewer products per encryption but exponentially
+    # larger tables (2048-bit key: win 16 = 2 x 1.28 GB, 45 -> 64 products per
+    # prime; win 20 = 2 x 16.6 GB, 52; win 22 = 2 x 59.9 GB, 47). The tables
+    # are rebuilt per key (keys are regenerated per fit(), label_trainer.py:137),
+    # so the window follows the volume a key has encrypted: 16 first, 20 after
+    # WIN_STEPS[0] elements, 22 after WIN_STEPS[1] - each step only when the
+    # new tables leave WIN_MARGIN bytes of the device free. $XHE_WIN_BITS or
+    # set_device_window() pin a window instead.
+    WIN_STEPS = ((0, 16), (8_000_000, 20), (64_000_000, 22))
+    WIN_MARGIN = 32 << 30
+
+    def set_device_window(self, win_bits: Optional[int]):
+        """Pin the fixed-base window (None: back to the volume policy). Cached
+        device keys are rebuilt on next use."""
+        self._win_pinned = win_bits
+        self._dev = {}
+
+    def _wanted_window(self):
+        pinned = getattr(self, "_win_pinned", None) or int(os.environ.get("XHE_WIN_BITS", "0") or 0)
+        if pinned:
+            return pinned
+        vol = getattr(self, "_volume", 0)
+        return max(w for thr, w in self.WIN_STEPS if vol >= thr)
+
+    def note_encrypt_volume(self, count: int):
+        """Called by the batched encryptions: the policy's element counter."""
+        self._volume = getattr(self, "_volume", 0) + int(count)
+
     def device_key(self, device: int = 0):
-        """Device-resident key for this context (built once, cached)."""
+        """Device-resident key for this context on `device` (built once, cached;
+        rebuilt with wider tables when the window policy asks for them)."""
         dev = getattr(self, "_dev", None)
         if dev is None:
             dev = self._dev = {}
         k = dev.get(device)
-        if k is None:
-            from .._native import DeviceKey
+        fixed_base = self.__is_private and self.djn_on
+        if k is not None and (not fixed_base or k.win_bits >= self._wanted_window()):
+            return k
+        with _KEY_LOCK:
+            k = dev.get(device)
+            want = self._wanted_window() if fixed_base else 0
+            if k is not None and (not fixed_base or k.win_bits >= want):
+                return k
+            from .._native import DeviceKey, device_free_bytes, table_bytes
             bits = device_key_bits(self.__n)
             h = self.h_pow_n if self.djn_on else None
+            if fixed_base:
+                have = table_bytes(bits, k.win_bits) if k is not None else 0
+                free = device_free_bytes(device)
+                while want > 16 and free is not None and table_bytes(bits, want) + self.WIN_MARGIN > free + have:
+                    want -= 2
+                if k is not None and k.win_bits >= want:
+                    return k
+                dev.pop(device, None)
+                k = None  # free the old tables before building the new ones
             if self.__is_private:
-                k = DeviceKey(bits, self.__n, self.__p, self.__q, h, device=device)
+                k = DeviceKey(bits, self.__n, self.__p, self.__q, h, device=device, win_bits=want)
             else:
                 k = DeviceKey(bits, self.__n, None, None, h, device=device)
             dev[device] = k
         return k
+
+    @staticmethod
+    def shard_devices(num_cores: int = -1):
+        """GPUs a batch is spread over (the reference spreads it over
+        get_core_num(num_cores) processes, paillier.py:321-332,388-394):
+        $XHE_DEVICES (comma-separated ids, may repeat; "all") if set, else
+        num_cores == -1 -> every visible GPU, num_cores = k -> the first k."""
+        spec = os.environ.get("XHE_DEVICES", "").strip()
+        if spec and spec != "all":
+            return [int(d) for d in spec.split(",") if d.strip()]
+        from .._native import visible_devices
+        n = visible_devices()
+        if spec == "all" or num_cores is None or num_cores < 1:
+            k = n
+        else:
+            k = min(int(num_cores), n)
+        return list(range(max(1, k)))

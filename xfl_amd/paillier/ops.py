@@ -1,22 +1,38 @@
-"""Batched device operations behind the drop-in API.
+"""Batched device operations behind the drop-in API, on flat word buffers.
 
-Every function takes/returns Python ints (the reference's mpz role) and runs
-the arithmetic on the GPU through the xhe C ABI (include/xhe.h). There is no
-CPU arithmetic path: a missing library or GPU raises from xfl_amd._native.
+Ciphertexts travel as C-contiguous uint32 [count, n2w] little-endian words
+plus int32 [count] exponents (the PaillierArray layout, include/xhe.h); the
+`*_words` functions take and return those buffers and never build Python
+ints. The int-list forms at the bottom serve single-element operations
+(PaillierCiphertext) and convert at the edge.
+
+Element-independent operations (encrypt, decrypt, add, scalar mul,
+obfuscate) are split over the context's shard devices (PaillierContext.
+shard_devices: num_cores / $XHE_DEVICES, the reference's process pool,
+paillier.py:321-332,388-394): contiguous element ranges, one host thread and
+one key handle per device, each writing its own slice of the output. There is
+no CPU arithmetic path: a missing library or GPU raises from xfl_amd._native.
 """
+import concurrent.futures
 import ctypes
 import itertools
 import os
+import threading
 
 import numpy as np
 
 from .. import _native as nat
 
 _nonce = itertools.count(1)
+_nonce_lock = threading.Lock()
+_pool = None
+MIN_SHARD = 1 << 16  # elements per device below which a call stays on one device
 
 
 def _seed():
-    return os.urandom(32), next(_nonce)
+    with _nonce_lock:
+        n = next(_nonce)
+    return os.urandom(32), n
 
 
 def _u32(a):
@@ -27,168 +43,320 @@ def _i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
-def _vp(a):
-    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+def _vp(a, row=0):
+    """pointer to row `row` of a C-contiguous array (None for None)"""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data + row * (a.strides[0] if a.ndim else 0))
 
 
-def encrypt_floats(ctx, xs, precision, max_exponent, obfuscation):
-    """encode (device) + encrypt for float64 values -> (raw ints, exponents, status)."""
-    dk = ctx.device_key()
-    x = np.ascontiguousarray(xs, dtype=np.float64)
+def _executor():
+    global _pool
+    if _pool is None:
+        _pool = concurrent.futures.ThreadPoolExecutor(max_workers=16, thread_name_prefix="xhe-shard")
+    return _pool
+
+
+def sharded(ctx, count, body, num_cores=-1):
+    """Run body(device_key, lo, hi) over contiguous slices of [0, count), one
+    slice per shard device (ctypes releases the GIL, so the devices run
+    concurrently). Small batches stay on the first device."""
+    devs = ctx.shard_devices(num_cores)
+    k = max(1, min(len(devs), count // MIN_SHARD))
+    if k == 1:
+        body(ctx.device_key(devs[0]), 0, count)
+        return
+    keys = [ctx.device_key(d) for d in devs[:k]]  # built here, not concurrently
+    bounds = [count * i // k for i in range(k + 1)]
+    futs = [_executor().submit(body, keys[i], bounds[i], bounds[i + 1]) for i in range(k)]
+    for f in futs:
+        f.result()
+
+
+def nw_of(ctx):
+    """32-bit words of m (the device key's nw: key size class of n / 32)"""
+    from .context import device_key_bits
+    return device_key_bits(ctx.n) // 32
+
+
+def n2w_of(ctx):
+    """32-bit words of a ciphertext (the device key's n2w)"""
+    return 2 * nw_of(ctx)
+
+
+# ------------------------------------------------------------ encryption
+def encrypt_floats_words(ctx, xs, precision, max_exponent, obfuscation, num_cores=-1):
+    """Paillier.encrypt over float64 values (paillier.py:273-339): device
+    encode + ChaCha20 draws + encrypt -> (ct words, exponents, status)."""
+    x = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1)
     n = x.shape[0]
-    ct = np.empty((n, dk.n2w), dtype=np.uint32)
+    n2w = n2w_of(ctx)
+    ct = np.empty((n, n2w), dtype=np.uint32)
     ex = np.empty(n, dtype=np.int32)
     st = np.empty(n, dtype=np.int32)
     if n == 0:
-        return [], ex, st
-    seed, nonce = _seed()
+        return ct, ex, st
     prec = -1 if precision is None else int(precision)
     has_max = max_exponent is not None
-    nat.check(nat.lib().xhe_encrypt_f64_host(dk.handle, _vp(x), n, prec, int(has_max),
-                                             int(max_exponent) if has_max else 0, int(bool(obfuscation)),
-                                             seed, nonce, _vp(ct), _vp(ex), _vp(st)), "encrypt")
-    return nat.words_to_ints(ct), ex, st
+    if obfuscation:
+        ctx.note_encrypt_volume(n)
+
+    def body(dk, lo, hi):
+        seed, nonce = _seed()  # fresh draws per shard
+        nat.check(nat.lib().xhe_encrypt_f64_host(dk.handle, _vp(x, lo), hi - lo, prec, int(has_max),
+                                                 int(max_exponent) if has_max else 0, int(bool(obfuscation)),
+                                                 seed, nonce, _vp(ct, lo), _vp(ex, lo), _vp(st, lo)), "encrypt")
+    sharded(ctx, n, body, num_cores)
+    return ct, ex, st
 
 
-def encrypt_encoded(ctx, ms, obfuscation):
-    """encrypt already-encoded integers m (0 <= m < n)."""
-    dk = ctx.device_key()
-    n = len(ms)
+def encrypt_encoded_words(ctx, mw, obfuscation, num_cores=-1):
+    """encrypt already-encoded integers m (0 <= m < n, nw words each)."""
+    mw = _u32(mw)
+    n = mw.shape[0]
+    ct = np.empty((n, n2w_of(ctx)), dtype=np.uint32)
     if n == 0:
-        return []
-    mw = nat.ints_to_words(ms, dk.nw)
-    ct = np.empty((n, dk.n2w), dtype=np.uint32)
-    seed, nonce = _seed()
-    nat.check(nat.lib().xhe_encrypt_words_host(dk.handle, _vp(mw), n, int(bool(obfuscation)), seed, nonce,
-                                               _vp(ct)), "encrypt")
-    return nat.words_to_ints(ct)
+        return ct
+    if obfuscation:
+        ctx.note_encrypt_volume(n)
+
+    def body(dk, lo, hi):
+        seed, nonce = _seed()
+        nat.check(nat.lib().xhe_encrypt_words_host(dk.handle, _vp(mw, lo), hi - lo, int(bool(obfuscation)), seed,
+                                                   nonce, _vp(ct, lo)), "encrypt")
+    sharded(ctx, n, body, num_cores)
+    return ct
 
 
-def decrypt_ints(ctx, raws):
-    """decrypt -> encoded integers m (paillier.py:347-365)."""
-    dk = ctx.device_key()
-    if len(raws) == 0:
-        return []
-    return nat.words_to_ints(dk.decrypt_words(nat.ints_to_words(raws, dk.n2w)))
+def obfuscate_words(ctx, cw, num_cores=-1):
+    """PaillierCiphertext.obfuscate for a batch: c * X, X a fresh obfuscator
+    (an encryption of 0), paillier.py:189-232."""
+    cw = _u32(cw)
+    n = cw.shape[0]
+    if n == 0:
+        return cw.copy()
+    xs = encrypt_encoded_words(ctx, np.zeros((n, nw_of(ctx)), dtype=np.uint32), True, num_cores)
+    z = np.zeros(n, dtype=np.int32)
+    return add_words(ctx, cw, z, xs, z, num_cores)[0]
 
 
-def decrypt_float32(ctx, raws, exps):
-    """decrypt + decode + float32 on the device -> (f64, f32, status)."""
-    dk = ctx.device_key()
-    n = len(raws)
-    cw = nat.ints_to_words(raws, dk.n2w)
+# ------------------------------------------------------------ decryption
+def decrypt_words(ctx, cw, num_cores=-1):
+    """decrypt -> encoded m words (paillier.py:347-365)."""
+    cw = _u32(cw)
+    n = cw.shape[0]
+    out = np.empty((n, nw_of(ctx)), dtype=np.uint32)
+    if n == 0:
+        return out
+
+    def body(dk, lo, hi):
+        nat.check(nat.lib().xhe_decrypt_host(dk.handle, _vp(cw, lo), hi - lo, _vp(out, lo)), "decrypt")
+    sharded(ctx, n, body, num_cores)
+    return out
+
+
+def decrypt_decode_words(ctx, cw, exps, num_cores=-1, want_m=False):
+    """decrypt + decode + float32 on the device -> (f64, f32, status[, m])
+    (paillier.py:370-398, encoder.py:56-64)."""
+    cw = _u32(cw)
     e = _i32(exps)
+    n = cw.shape[0]
     f64 = np.empty(n, dtype=np.float64)
     f32 = np.empty(n, dtype=np.float32)
     st = np.empty(n, dtype=np.int32)
+    m = np.empty((n, nw_of(ctx)), dtype=np.uint32) if want_m else None
     if n:
-        nat.check(nat.lib().xhe_decrypt_decode_host(dk.handle, _vp(cw), _vp(e), n, _vp(f64), _vp(f32), _vp(st),
-                                                    None), "decrypt")
-    return f64, f32, st
+        def body(dk, lo, hi):
+            nat.check(nat.lib().xhe_decrypt_decode_host(dk.handle, _vp(cw, lo), _vp(e, lo), hi - lo, _vp(f64, lo),
+                                                        _vp(f32, lo), _vp(st, lo), _vp(m, lo)), "decrypt")
+        sharded(ctx, n, body, num_cores)
+    return (f64, f32, st, m) if want_m else (f64, f32, st)
+
+
+# ------------------------------------------------------------ homomorphic ops
+def add_words(ctx, aw, ea, bw, eb, num_cores=-1):
+    """ciphertext + ciphertext with exponent alignment (paillier.py:79-123)
+    -> (words, exponents)."""
+    aw, bw = _u32(aw), _u32(bw)
+    ea, eb = _i32(ea), _i32(eb)
+    n = aw.shape[0]
+    out = np.empty_like(aw)
+    eo = np.empty(n, dtype=np.int32)
+    if n == 0:
+        return out, eo
+    dmax = int(np.max(np.abs(ea.astype(np.int64) - eb.astype(np.int64))))
+
+    def body(dk, lo, hi):
+        nat.check(nat.lib().xhe_mulmod_host(dk.handle, _vp(aw, lo), _vp(ea, lo), _vp(bw, lo), _vp(eb, lo), hi - lo,
+                                            dmax, _vp(out, lo), _vp(eo, lo)), "add")
+    sharded(ctx, n, body, num_cores)
+    return out, eo
+
+
+def powmod_words(ctx, cw, kw_, kbits, invert_first=False, num_cores=-1):
+    """c^k (or (c^-1)^k) mod n^2 per element; k as [count, kw] words."""
+    cw = _u32(cw)
+    kw_ = _u32(kw_)
+    n = cw.shape[0]
+    out = np.empty_like(cw)
+    if n == 0:
+        return out
+    kwords = kw_.shape[1]
+
+    def body(dk, lo, hi):
+        nat.check(nat.lib().xhe_powmod_host(dk.handle, _vp(cw, lo), _vp(kw_, lo), kwords, int(kbits), hi - lo,
+                                            int(bool(invert_first)), _vp(out, lo)), "powmod")
+    sharded(ctx, n, body, num_cores)
+    return out
+
+
+def raw_mul_words(ctx, cw, kabs, neg, num_cores=-1):
+    """PaillierCiphertext._raw_mul (paillier.py:156-187) for encoded scalars
+    given as |k| with a sign: a positive k gives c^k; a negative scalar
+    (encoded n - |k|, >= min_value_for_negative) gives inv(c)^|k|.
+    kabs: int64 array (|k| < 2^63) or [count, kw] uint32 words."""
+    cw = _u32(cw)
+    n = cw.shape[0]
+    out = np.empty_like(cw)
+    if n == 0:
+        return out
+    if isinstance(kabs, np.ndarray) and kabs.ndim == 1:
+        kabs = np.ascontiguousarray(kabs, dtype=np.uint64)
+        kw_ = kabs.view(np.uint32).reshape(n, 2)
+        kbits = max(1, int(kabs.max()).bit_length())
+    else:
+        kw_ = _u32(kabs)
+        kbits = max(1, max(nat.words_to_ints(kw_)).bit_length()) if n else 1
+    neg = np.asarray(neg, dtype=bool).reshape(-1)
+    for flag in (False, True):
+        idx = np.nonzero(neg == flag)[0]
+        if idx.size == 0:
+            continue
+        if idx.size == n:
+            out[:] = powmod_words(ctx, cw, kw_, kbits, flag, num_cores)
+        else:
+            out[idx] = powmod_words(ctx, cw[idx], kw_[idx], kbits, flag, num_cores)
+    return out
+
+
+def segment_sums_words(ctx, cw, exps, seg_begin):
+    """Homomorphic sums of consecutive segments: segment s covers
+    [seg_begin[s], seg_begin[s+1]); result exponent = min exponent of the
+    segment (paillier.py:106-123 folded; order-free). An empty
+    segment gives 1 with exponent 0."""
+    seg = np.ascontiguousarray(seg_begin, dtype=np.int64)
+    nseg = seg.shape[0] - 1
+    cw = _u32(cw)
+    n = cw.shape[0]
+    e = np.asarray(exps, dtype=np.int64).reshape(-1)
+    lens = np.diff(seg)
+    emin = np.zeros(nseg, dtype=np.int64)
+    nz = lens > 0
+    if n:
+        emin[nz] = np.minimum.reduceat(e, seg[:-1][nz])
+    d = (e - np.repeat(emin, lens)).astype(np.int32)
+    dmax = int(d.max()) if n else 0
+    n2w = n2w_of(ctx)
+    src = cw if n else np.zeros((1, n2w), dtype=np.uint32)
+    out = np.empty((nseg, n2w), dtype=np.uint32)
+    dk = ctx.device_key()
+    nat.check(nat.lib().xhe_segprod_host(dk.handle, _vp(src), _vp(d) if dmax else None, dmax, n, _vp(seg), nseg,
+                                         _vp(out)), "segprod")
+    return out, emin.astype(np.int32)
+
+
+def multiexp_words(ctx, bw, idx, kw_, kbits, win_bits=0):
+    """out[j] = prod_t bases[idx[j][t]]^k[j][t] mod n^2 (k >= 0, [ncols,
+    nterms, kw] words): one xhe_multiexp call (Straus windows, per-base tables
+    shared by all j)."""
+    bw = _u32(bw)
+    iw = np.ascontiguousarray(idx, dtype=np.int32)
+    ncols, nterms = iw.shape
+    kw_ = _u32(kw_).reshape(ncols * nterms, -1)
+    if ncols == 0 or nterms == 0 or bw.shape[0] == 0:
+        raise ValueError("multiexp: empty problem")
+    out = np.empty((ncols, n2w_of(ctx)), dtype=np.uint32)
+    dk = ctx.device_key()
+    nat.check(nat.lib().xhe_multiexp_host(dk.handle, _vp(bw), bw.shape[0], _vp(iw), _vp(kw_), kw_.shape[1],
+                                          int(kbits), ncols, nterms, int(win_bits), _vp(out)), "multiexp")
+    return out
+
+
+# ------------------------------------------------------------ int forms
+def encrypt_floats(ctx, xs, precision, max_exponent, obfuscation):
+    """-> (raw ints, exponents, status)"""
+    ct, ex, st = encrypt_floats_words(ctx, xs, precision, max_exponent, obfuscation)
+    return (nat.words_to_ints(ct) if ct.shape[0] else []), ex, st
+
+
+def encrypt_encoded(ctx, ms, obfuscation):
+    if len(ms) == 0:
+        return []
+    return nat.words_to_ints(encrypt_encoded_words(ctx, nat.ints_to_words(ms, nw_of(ctx)), obfuscation))
+
+
+def decrypt_ints(ctx, raws):
+    if len(raws) == 0:
+        return []
+    return nat.words_to_ints(decrypt_words(ctx, nat.ints_to_words(raws, n2w_of(ctx))))
+
+
+def decrypt_float32(ctx, raws, exps):
+    """-> (f64, f32, status)"""
+    n2w = n2w_of(ctx)
+    cw = nat.ints_to_words(raws, n2w) if len(raws) else np.zeros((0, n2w), dtype=np.uint32)
+    return decrypt_decode_words(ctx, cw, exps)
 
 
 def add(ctx, ra, ea, rb, eb):
-    """ciphertext + ciphertext with exponent alignment -> (raws, exps)."""
-    dk = ctx.device_key()
-    n = len(ra)
-    if n == 0:
+    if len(ra) == 0:
         return [], np.empty(0, dtype=np.int32)
-    aw = nat.ints_to_words(ra, dk.n2w)
-    bw = nat.ints_to_words(rb, dk.n2w)
-    ea = _i32(ea)
-    eb = _i32(eb)
-    dmax = int(np.max(np.abs(ea.astype(np.int64) - eb.astype(np.int64)))) if n else 0
-    out = np.empty((n, dk.n2w), dtype=np.uint32)
-    eo = np.empty(n, dtype=np.int32)
-    nat.check(nat.lib().xhe_mulmod_host(dk.handle, _vp(aw), _vp(ea), _vp(bw), _vp(eb), n, dmax, _vp(out),
-                                        _vp(eo)), "add")
+    n2w = n2w_of(ctx)
+    out, eo = add_words(ctx, nat.ints_to_words(ra, n2w), ea, nat.ints_to_words(rb, n2w), eb)
     return nat.words_to_ints(out), eo
 
 
 def powmod(ctx, raws, ks, invert_first=False):
-    """c^k (or (c^-1)^k) mod n^2 for per-element k >= 0."""
-    dk = ctx.device_key()
-    n = len(raws)
-    if n == 0:
+    if len(raws) == 0:
         return []
     kbits = max(int(k).bit_length() for k in ks)
     kw = max(1, (kbits + 31) // 32)
-    cw = nat.ints_to_words(raws, dk.n2w)
-    kwds = nat.ints_to_words(ks, kw)
-    out = np.empty((n, dk.n2w), dtype=np.uint32)
-    nat.check(nat.lib().xhe_powmod_host(dk.handle, _vp(cw), _vp(kwds), kw, kbits, n, int(bool(invert_first)),
-                                        _vp(out)), "powmod")
+    out = powmod_words(ctx, nat.ints_to_words(raws, n2w_of(ctx)), nat.ints_to_words(ks, kw), kbits, invert_first)
     return nat.words_to_ints(out)
 
 
 def raw_mul(ctx, raws, ks):
-    """PaillierCiphertext._raw_mul for 0 <= k < n (paillier.py:156-187):
-    inv(c)^(n-k) when k >= min_value_for_negative, else c^k."""
-    n = len(raws)
-    out = [None] * n
-    thr = ctx.min_value_for_negative
-    pos = [i for i in range(n) if ks[i] < thr]
-    neg = [i for i in range(n) if ks[i] >= thr]
-    if pos:
-        r = powmod(ctx, [raws[i] for i in pos], [ks[i] for i in pos])
-        for i, v in zip(pos, r):
-            out[i] = v
-    if neg:
-        r = powmod(ctx, [raws[i] for i in neg], [ctx.n - ks[i] for i in neg], invert_first=True)
-        for i, v in zip(neg, r):
-            out[i] = v
-    return out
-
-
-def obfuscate(ctx, raws):
-    """PaillierCiphertext.obfuscate: c * X with X a fresh obfuscator (= encryption of 0)."""
+    """_raw_mul for encoded k in [0, n): inv(c)^(n-k) when k >=
+    min_value_for_negative, else c^k."""
     n = len(raws)
     if n == 0:
         return []
-    xs = encrypt_encoded(ctx, [0] * n, True)
-    z = np.zeros(n, dtype=np.int32)
-    r, _ = add(ctx, raws, z, xs, z)
-    return r
-
-
-def multiexp(ctx, bases, idx, ks, win_bits=0):
-    """out[j] = prod_t bases[idx[j][t]]^ks[j][t] mod n^2 (ks >= 0): one
-    xhe_multiexp call (Straus windows, per-base tables shared by all j)."""
-    dk = ctx.device_key()
-    ncols = len(idx)
-    nterms = len(idx[0]) if ncols else 0
-    if ncols == 0 or nterms == 0 or not bases:
-        raise ValueError("multiexp: empty problem")
-    flat_k = [int(k) for row in ks for k in row]
-    kbits = max(1, max(k.bit_length() for k in flat_k))
-    kw = (kbits + 31) // 32
-    bw = nat.ints_to_words(bases, dk.n2w)
-    iw = np.ascontiguousarray(idx, dtype=np.int32).reshape(ncols, nterms)
-    kwds = nat.ints_to_words(flat_k, kw)
-    out = np.empty((ncols, dk.n2w), dtype=np.uint32)
-    nat.check(nat.lib().xhe_multiexp_host(dk.handle, _vp(bw), len(bases), _vp(iw), _vp(kwds), kw, kbits, ncols,
-                                          nterms, int(win_bits), _vp(out)), "multiexp")
+    thr = ctx.min_value_for_negative
+    neg = np.array([k >= thr for k in ks], dtype=bool)
+    kabs = [ctx.n - k if g else k for k, g in zip(ks, neg)]
+    kbits = max(1, max(int(k).bit_length() for k in kabs))
+    out = raw_mul_words(ctx, nat.ints_to_words(raws, n2w_of(ctx)), nat.ints_to_words(kabs, (kbits + 31) // 32), neg)
     return nat.words_to_ints(out)
 
 
+def obfuscate(ctx, raws):
+    if len(raws) == 0:
+        return []
+    return nat.words_to_ints(obfuscate_words(ctx, nat.ints_to_words(raws, n2w_of(ctx))))
+
+
 def segment_sums(ctx, raws, exps, seg_begin):
-    """Homomorphic sums of consecutive segments: segment s covers
-    [seg_begin[s], seg_begin[s+1]); result exponent = min exponent of the
-    segment (paillier.py:106-123 folded; order-free)."""
-    dk = ctx.device_key()
-    seg = np.ascontiguousarray(seg_begin, dtype=np.int64)
-    nseg = seg.shape[0] - 1
-    n = len(raws)
-    e = np.asarray(exps, dtype=np.int64)
-    emin = np.zeros(nseg, dtype=np.int64)
-    d = np.zeros(n, dtype=np.int32)
-    for s in range(nseg):
-        lo, hi = int(seg[s]), int(seg[s + 1])
-        if hi > lo:
-            emin[s] = e[lo:hi].min()
-            d[lo:hi] = (e[lo:hi] - emin[s]).astype(np.int32)
-    dmax = int(d.max()) if n else 0
-    cw = nat.ints_to_words(raws, dk.n2w) if n else np.zeros((1, dk.n2w), dtype=np.uint32)
-    out = np.empty((nseg, dk.n2w), dtype=np.uint32)
-    nat.check(nat.lib().xhe_segprod_host(dk.handle, _vp(cw), _vp(d), dmax, n, _vp(seg), nseg, _vp(out)), "segprod")
+    n2w = n2w_of(ctx)
+    cw = nat.ints_to_words(raws, n2w) if len(raws) else np.zeros((0, n2w), dtype=np.uint32)
+    out, emin = segment_sums_words(ctx, cw, exps, seg_begin)
     return nat.words_to_ints(out), emin
+
+
+def multiexp(ctx, bases, idx, ks, win_bits=0):
+    flat_k = [int(k) for row in ks for k in row]
+    kbits = max(1, max(k.bit_length() for k in flat_k))
+    kw = (kbits + 31) // 32
+    ncols = len(idx)
+    out = multiexp_words(ctx, nat.ints_to_words(bases, n2w_of(ctx)), np.asarray(idx, dtype=np.int32).reshape(ncols, -1),
+                         nat.ints_to_words(flat_k, kw), kbits, win_bits)
+    return nat.words_to_ints(out)

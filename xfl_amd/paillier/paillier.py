@@ -10,6 +10,7 @@ from typing import Optional, Union
 
 import numpy as np
 
+from .. import _native as nat
 from . import ops
 from .context import PaillierContext
 from .encoder import PaillierEncoder, int_to_float_gmpy
@@ -185,14 +186,6 @@ def raws_of(cts):
     return [c.raw_ciphertext for c in cts]
 
 
-def _to_ciphertexts(context, raws, exps, shape):
-    from .array import PaillierArray
-    out = np.empty(len(raws), dtype=object)
-    for i, (r, e) in enumerate(zip(raws, exps)):
-        out[i] = PaillierCiphertext(context, r, int(e))
-    return out.reshape(shape).view(PaillierArray)
-
-
 def _encode_ints(context, xs, precision, max_exponent):
     """Reference per-element encode for integer elements (encoder.py:29-54)."""
     ms, es = [], []
@@ -218,16 +211,20 @@ class Paillier(object):
 
     @staticmethod
     def serialize(data: Union[np.ndarray, PaillierCiphertext], compression: bool = True) -> bytes:
-        """paillier.py:244-258"""
+        """paillier.py:244-258: the pickle of an ndarray[object] of
+        RawCiphertext, written natively from the flat words (wire.hpp)."""
         from ..compat import compress, dumps
+        from . import wire
+        from .array import PaillierArray
         if isinstance(data, PaillierCiphertext):
             return data.serialize(compression)
-
+        if isinstance(data, PaillierArray):
+            out = wire.encode_words(data.words, data.exponents, data.shape)
+            return compress(out) if compression else out
         if isinstance(data, np.ndarray) and data.dtype == object:
             flat = list(data.reshape(-1))
             materialize(flat)
             if flat and all(isinstance(x, PaillierCiphertext) for x in flat):
-                from . import wire
                 raws = [x.raw_ciphertext for x in flat]
                 ctx = flat[0].context
                 bits = ctx.n_square.bit_length() if ctx is not None else max(r.bit_length() for r in raws)
@@ -242,19 +239,16 @@ class Paillier(object):
 
     @staticmethod
     def ciphertext_from(context: PaillierContext, data: bytes, compression: bool = True):
-        """paillier.py:260-271"""
+        """paillier.py:260-271 -> PaillierArray (context may be None, as in
+        label_trainer.py:258; pass the key to decrypt)."""
         from ..compat import decompress, loads
         from .array import PaillierArray
         if compression:
             data = decompress(data)
-        try:  # native decode of the ciphertext-array format
+        try:  # native decode of the ciphertext-array format, straight into words
             from . import wire
-            n2w = (context.n_square.bit_length() + 31) // 32 if context is not None else None
-            raws, exps, shape = wire.decode(data, n2w)
-            out = np.empty(len(raws), dtype=object)
-            for i, (r, e) in enumerate(zip(raws, exps.tolist())):
-                out[i] = PaillierCiphertext(context, r, e)
-            return out.reshape(shape).view(PaillierArray)
+            w, e, shape = wire.decode_words(data, ops.n2w_of(context) if context is not None else None)
+            return PaillierArray.from_buffers(context, w, e, shape)
         except ValueError:
             pass
         unpickled = loads(data)
@@ -262,26 +256,32 @@ class Paillier(object):
         def f(x):
             return PaillierCiphertext(context, int(x.value), x.exp)
 
-        return np.vectorize(f, otypes=[PaillierCiphertext])(unpickled).view(PaillierArray)
+        return PaillierArray(np.vectorize(f, otypes=[PaillierCiphertext])(unpickled), context=context)
 
     @classmethod
     def encrypt(cls, context: PaillierContext, data: Union[int, float, np.ndarray], precision: Optional[int] = None,
                 max_exponent: Optional[int] = None, obfuscation: bool = True,
                 num_cores: int = -1) -> Union[PaillierCiphertext, np.ndarray]:
-        """paillier.py:289-339. num_cores is accepted for compatibility; the
-        elements are spread over GPU lanes instead of processes."""
+        """paillier.py:289-339. Arrays come back as a PaillierArray (flat
+        words + exponents, ciphertext objects on element access); num_cores
+        spreads the elements over GPUs (PaillierContext.shard_devices) where
+        the reference spreads them over processes."""
+        from .array import PaillierArray
         if isinstance(data, np.ndarray):
             shape = data.shape
             flat = data.reshape(-1)
             n = flat.shape[0]
-            raws = [None] * n
-            exps = [0] * n
             if flat.dtype.kind == "f":
-                r, e, st = ops.encrypt_floats(context, flat.astype(np.float64), precision, max_exponent, obfuscation)
+                w, e, st = ops.encrypt_floats_words(context, flat, precision, max_exponent, obfuscation, num_cores)
                 Paillier._raise_status(st)
-                raws, exps = r, e
+                return PaillierArray.from_buffers(context, w, e, shape)
+            nw = ops.nw_of(context)
+            mw = np.zeros((n, nw), dtype=np.uint32)
+            exps = np.zeros(n, dtype=np.int32)
+            fl_idx, int_idx = [], []
+            if flat.dtype.kind in "iub":
+                int_idx = range(n)
             else:
-                fl_idx, int_idx = [], []
                 for i, x in enumerate(flat):
                     if isinstance(x, (float, np.floating)):
                         fl_idx.append(i)
@@ -290,18 +290,20 @@ class Paillier(object):
                     else:
                         PaillierEncoder.cal_exponent(x, precision)  # raises TypeError like the reference
                         raise TypeError(f"Unsupported data type {type(x)}")
-                if fl_idx:
-                    r, e, st = ops.encrypt_floats(context, np.array([float(flat[i]) for i in fl_idx]), precision,
-                                                  max_exponent, obfuscation)
-                    Paillier._raise_status(st)
-                    for j, i in enumerate(fl_idx):
-                        raws[i], exps[i] = r[j], int(e[j])
-                if int_idx:
-                    ms, es = _encode_ints(context, [flat[i] for i in int_idx], precision, max_exponent)
-                    r = ops.encrypt_encoded(context, ms, obfuscation)
-                    for j, i in enumerate(int_idx):
-                        raws[i], exps[i] = r[j], es[j]
-            return _to_ciphertexts(context, raws, exps, shape)
+            words = np.empty((n, ops.n2w_of(context)), dtype=np.uint32)
+            if len(fl_idx):
+                fi = np.asarray(fl_idx, dtype=np.int64)
+                w, e, st = ops.encrypt_floats_words(context, np.array([float(flat[i]) for i in fl_idx]), precision,
+                                                    max_exponent, obfuscation, num_cores)
+                Paillier._raise_status(st)
+                words[fi] = w
+                exps[fi] = e
+            if len(int_idx):
+                ii = np.asarray(int_idx, dtype=np.int64)
+                ms, es = _encode_ints(context, [flat[i] for i in int_idx], precision, max_exponent)
+                words[ii] = ops.encrypt_encoded_words(context, nat.ints_to_words(ms, nw), obfuscation, num_cores)
+                exps[ii] = es
+            return PaillierArray.from_buffers(context, words, exps, shape)
         elif isinstance(data, (int, float)):
             if isinstance(data, float):
                 r, e, st = ops.encrypt_floats(context, np.array([data]), precision, max_exponent, obfuscation)
@@ -333,15 +335,28 @@ class Paillier(object):
     def decrypt(cls, context: PaillierContext, data: Union[PaillierCiphertext, np.ndarray], dtype: str = 'float',
                 num_cores: int = -1, out_origin: bool = False):
         """paillier.py:370-417"""
+        from .array import PaillierArray
         if not context.is_private():
             raise TypeError("Try to decrypt a paillier ciphertext by a public key.")
+        if isinstance(data, PaillierArray):
+            arr = data._aligned_words(ops.n2w_of(context))
+            if not out_origin and dtype == 'float':
+                # decrypt + decode + float32 on the device, straight from the words
+                _, f32, st = ops.decrypt_decode_words(context, arr.words, arr.exponents, num_cores)
+                if np.any(st != 0):
+                    raise OverflowError("Overflow detected during decoding encrypted number.")
+                return f32.reshape(arr.shape)
+            ms = nat.words_to_ints(ops.decrypt_words(context, arr.words, num_cores)) if arr.size else []
+            vals = [PaillierEncoder.decode_single(context, m, int(e)) for m, e in zip(ms, arr.exponents.tolist())]
+            out = np.empty(len(vals), dtype=object)
+            out[:] = vals
+            return _finish_decrypt(out.reshape(arr.shape), dtype, out_origin)
         if isinstance(data, np.ndarray):
             shape = data.shape
             flat = data.reshape(-1)
             idx = [i for i, x in enumerate(flat) if isinstance(x, PaillierCiphertext)]
             if not out_origin and dtype == 'float' and len(idx) == len(flat) and len(flat) > 0:
-                _, f32, st = ops.decrypt_float32(context, raws_of(list(flat)),
-                                                 [x.exponent for x in flat])
+                _, f32, st = ops.decrypt_float32(context, raws_of(list(flat)), [x.exponent for x in flat])
                 if np.any(st != 0):
                     raise OverflowError("Overflow detected during decoding encrypted number.")
                 return f32.reshape(shape)
@@ -351,16 +366,7 @@ class Paillier(object):
                 vals[i] = PaillierEncoder.decode_single(context, m, flat[i].exponent)
             out = np.empty(len(vals), dtype=object)
             out[:] = vals
-            out = out.reshape(shape)
-            if not out_origin:
-                if dtype == 'float':
-                    out = _astype_f32(out)
-                elif dtype == 'int':
-                    out = out.astype(np.int32)
-                else:
-                    warnings.warn(f"dtype {dtype} not supported.")
-                    out = _astype_f32(out)
-            return out
+            return _finish_decrypt(out.reshape(shape), dtype, out_origin)
         elif isinstance(data, PaillierCiphertext):
             out = cls._decrypt_single(data, context)
             if not out_origin:
@@ -378,14 +384,21 @@ class Paillier(object):
 
     @classmethod
     def obfuscate(cls, ciphertext: Union[PaillierCiphertext, np.ndarray]):
-        """paillier.py:419-431"""
+        """paillier.py:419-431: re-randomises the ciphertexts in place (the
+        reference calls c.obfuscate() on each element) and returns them."""
+        from .array import PaillierArray
+        if isinstance(ciphertext, PaillierArray):
+            ctx = ciphertext.context
+            if ciphertext.size:
+                if ctx is None:
+                    raise ValueError("ciphertext array without a context")
+                ciphertext.words[:] = ops.obfuscate_words(ctx, ciphertext._aligned_words(ops.n2w_of(ctx)).words)
+            return ciphertext
         if isinstance(ciphertext, np.ndarray):
             flat = ciphertext.reshape(-1)
             if not all(isinstance(c, PaillierCiphertext) for c in flat):
                 raise TypeError("Unsupported raw ciphertext type")
             if len(flat):
-                # re-randomise the caller's objects in place (c.obfuscate() per
-                # element in the reference), one batched call
                 ctx = flat[0].context
                 raws = ops.obfuscate(ctx, raws_of(list(flat)))
                 for c, r in zip(flat, raws):
@@ -395,6 +408,18 @@ class Paillier(object):
             return ciphertext.obfuscate()
         else:
             raise TypeError(f"Unsupported raw ciphertext type {type(ciphertext)}")
+
+
+def _finish_decrypt(out, dtype, out_origin):
+    """paillier.py:396-414: the array's dtype conversion after decode."""
+    if out_origin:
+        return out
+    if dtype == 'float':
+        return _astype_f32(out)
+    if dtype == 'int':
+        return out.astype(np.int32)
+    warnings.warn(f"dtype {dtype} not supported.")
+    return _astype_f32(out)
 
 
 def _astype_f32(obj_arr):

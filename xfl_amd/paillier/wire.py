@@ -20,27 +20,64 @@ def _vp(a):
 
 def encode(raws, exps, shape, n2w):
     """pickle bytes of the ndarray (shape) of RawCiphertext(raws[i], exps[i])."""
-    count = len(raws)
-    ct = nat.ints_to_words(raws, n2w) if count else np.zeros((1, n2w), np.uint32)
+    ct = nat.ints_to_words(raws, n2w) if len(raws) else np.zeros((0, n2w), np.uint32)
+    return encode_words(ct, exps, shape)
+
+
+def encode_words(ct, exps, shape):
+    """pickle bytes of the ndarray (shape) of RawCiphertext from flat buffers:
+    ct uint32 [count, n2w], exps int32 [count]."""
+    ct = np.ascontiguousarray(ct, dtype=np.uint32)
+    count, n2w = ct.shape
+    if count == 0:
+        ct = np.zeros((1, n2w), np.uint32)
     ex = np.ascontiguousarray(exps, dtype=np.int32) if count else np.zeros(1, np.int32)
     shp = np.ascontiguousarray(shape, dtype=np.int64) if len(shape) else np.zeros(1, np.int64)
     L = nat.lib()
     need = ctypes.c_int64()
-    cap = 256 + count * (4 * n2w + 24)
-    out = np.empty(cap, dtype=np.uint8)
-    rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), _vp(out), cap, ctypes.byref(need))
-    if rc == nat.XHE_EOVERFLOW:
-        out = np.empty(need.value, dtype=np.uint8)
-        rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), _vp(out), need.value,
-                               ctypes.byref(need))
+    rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), None, 0, ctypes.byref(need))
+    if rc != nat.XHE_EOVERFLOW:
+        nat.check(rc, "wire encode")
+    # written straight into the bytes object handed back (no staging copy of
+    # the ~0.5 KB/ciphertext payload); nothing else references it yet
+    out = bytes(need.value)
+    rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), ctypes.cast(out, ctypes.c_void_p),
+                           need.value, ctypes.byref(need))
     nat.check(rc, "wire encode")
-    return out[:need.value].tobytes()
+    return out
 
 
 def decode(data, n2w=None):
     """(raw ints, exponents, shape) of a ciphertext-array pickle; raises
     ValueError when the bytes are not that format."""
-    n2w = n2w or _MAX_WORDS
+    ct, ex, shape = _decode(data, n2w or _MAX_WORDS)
+    return (nat.words_to_ints(ct) if ct.shape[0] else []), ex, shape
+
+
+# word widths tried for a payload decoded without a context: n^2 of the
+# device key sizes (context.SUPPORTED_DEVICE_BITS), narrowest first
+_WIDTHS = (128, 192, 256, 512)
+
+
+def decode_words(data, n2w=None):
+    """(uint32 words [count, n2w], int32 exponents, shape) of a
+    ciphertext-array pickle. Without n2w the narrowest device width that
+    holds every value is used. Raises ValueError when the bytes are not that
+    format."""
+    if n2w is not None:
+        return _decode(data, n2w)
+    err = None
+    for w in _WIDTHS:
+        try:
+            return _decode(data, w)
+        except ValueError as e:  # "value too large" -> next width; anything else is final
+            err = e
+            if "too large" not in str(e):
+                raise
+    raise err
+
+
+def _decode(data, n2w):
     L = nat.lib()
     buf = np.frombuffer(data, dtype=np.uint8)
     count = ctypes.c_int64()
@@ -58,4 +95,4 @@ def decode(data, n2w=None):
     if rc != nat.XHE_OK:
         raise ValueError(nat.lib().xhe_last_error().decode(errors="replace"))
     n = count.value
-    return nat.words_to_ints(ct[:n]) if n else [], ex[:n], tuple(int(s) for s in shape[:ndim.value])
+    return ct[:n], ex[:n], tuple(int(s) for s in shape[:ndim.value])
