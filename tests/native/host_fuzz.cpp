@@ -141,7 +141,7 @@ static void roundtrip(std::mt19937_64& rng) {
 // Our own encoder's output: the fast decode path must accept it and agree
 // with the general pickle machine; then it is fuzzed like the other seeds.
 static void own_format(std::mt19937_64& rng) {
-  const int64_t counts[] = {0, 1, 5, 999, 1000, 1001, 2500};
+  const int64_t counts[] = {0, 1, 5, 999, 1000, 1001, 2500, 9001};
   for (int64_t count : counts) {
     const int n2w = 128;
     std::vector<uint32_t> ct((size_t)std::max<int64_t>(count, 1) * n2w);
@@ -153,10 +153,13 @@ static void own_format(std::mt19937_64& rng) {
       for (int k = top; k < n2w; ++k) ct[(size_t)i * n2w + k] = 0;
     }
     int64_t shape[2] = {count, 1};
-    for (int threads : {1, 3}) {
+    for (int threads : {1, 3, 16}) {
       int64_t need = xhe::wire::encode(ct.data(), ex.data(), count, n2w, shape, 2, nullptr, 0, threads);
       Bytes out((size_t)need);
       xhe::wire::encode(ct.data(), ex.data(), count, n2w, shape, 2, out.data(), need, threads);
+      Bytes ref((size_t)xhe::wire::encode_reference(ct.data(), ex.data(), count, n2w, shape, 2, nullptr, 0));
+      xhe::wire::encode_reference(ct.data(), ex.data(), count, n2w, shape, 2, ref.data(), (int64_t)ref.size());
+      if (ref != out) std::abort();  // the fast writer produces the specification's bytes
       const int64_t cap = std::max<int64_t>(count, 1);
       std::vector<uint32_t> a((size_t)cap * n2w), b((size_t)cap * n2w);
       std::vector<int32_t> ea(cap), eb(cap);

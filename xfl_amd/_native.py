@@ -51,8 +51,8 @@ SIGNATURES = {
                                     ctypes.c_int64, ctypes.c_int, _vp, _vp]),
     "xhe_multiexp_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp]),
-    "xhe_encrypt_host": (ctypes.c_int, [_vp, _u32p, _u32p, ctypes.c_int64, _u32p]),
-    "xhe_decrypt_host": (ctypes.c_int, [_vp, _u32p, ctypes.c_int64, _u32p]),
+    "xhe_encrypt_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp]),
+    "xhe_decrypt_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp]),
     "xhe_encrypt_f64_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, _vp, _vp, _vp]),
     "xhe_encrypt_words_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p,
@@ -125,6 +125,40 @@ def check(rc, what=""):
     if rc == XHE_EINVAL:
         raise ValueError(f"{what}: {msg}")
     raise XheError(f"{what} failed ({rc}): {msg}")
+
+
+# ------------------------------------------------------------ host buffers
+_libc = None
+_HUGE = 2 << 20
+_MADV_HUGEPAGE = 14
+
+
+def advise_huge(addr, nbytes):
+    """madvise(MADV_HUGEPAGE) on the 2 MiB-aligned interior of a fresh buffer:
+    the ciphertext payloads are hundreds of MB, and first-touch faults at 4 KiB
+    cost more than writing them (transparent hugepages are 'madvise' mode on
+    these hosts). Best effort: ignored where unsupported."""
+    global _libc
+    if nbytes < (32 << 20):
+        return
+    try:
+        if _libc is None:
+            _libc = ctypes.CDLL(None)
+            _libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        lo = (addr + _HUGE - 1) & ~(_HUGE - 1)
+        hi = (addr + nbytes) & ~(_HUGE - 1)
+        if hi > lo:
+            _libc.madvise(lo, hi - lo, _MADV_HUGEPAGE)
+    except (OSError, AttributeError):
+        pass
+
+
+def empty(shape, dtype):
+    """np.empty for large host buffers the library writes into (hugepage-backed)."""
+    a = np.empty(shape, dtype=dtype)
+    if a.nbytes >= (32 << 20):
+        advise_huge(a.ctypes.data, a.nbytes)
+    return a
 
 
 # ------------------------------------------------------------ int <-> words

@@ -204,6 +204,63 @@ inline void emit_footer(Writer& w) {
   w.put('.');
 }
 
+// Bytes of LONG1/LONG4 payload for a non-negative value (put_long's rule:
+// minimal two's complement, one sign bit of room).
+inline int64_t long_nbytes(const uint32_t* row, int nw) {
+  int top = nw - 1;
+  while (top >= 0 && row[top] == 0) --top;
+  if (top < 0) return 0;
+  const int64_t bits = 32 * (int64_t)top + (32 - __builtin_clz(row[top]));
+  return (bits + 8) / 8;
+}
+
+// Size of element i's bytes, as emit_elem writes them (i > 0: closed form).
+inline int64_t elem_bytes(const uint32_t* row, int n2w, int32_t e, int64_t i, int64_t count) {
+  if (i == 0) {
+    Writer w{nullptr, 0};
+    emit_elem(w, row, n2w, e, 0, count);
+    return w.n;
+  }
+  const int64_t nb = long_nbytes(row, n2w);
+  int64_t s = 8 + (nb < 256 ? 2 : 5) + nb + 2 + ((e >= 0 && e < 256) ? 2 : 5) + 2;
+  if (i % 1000 == 0) s += 1;
+  if (i % 1000 == 999 || i == count - 1) s += 1;
+  return s;
+}
+
+// emit_elem for i > 0 with direct stores (the hot loop of serialize).
+inline uint8_t* write_elem(uint8_t* d, const uint32_t* row, int n2w, int32_t e, int64_t i, int64_t count) {
+  static const uint8_t pre[8] = {'h', 1, ')', 0x81, '}', '(', 'h', 2};
+  if (i % 1000 == 0) *d++ = '(';
+  memcpy(d, pre, 8);
+  d += 8;
+  const int64_t nb = long_nbytes(row, n2w);
+  if (nb < 256) {
+    *d++ = 0x8a;
+    *d++ = (uint8_t)nb;
+  } else {
+    *d++ = 0x8b;
+    for (int k = 0; k < 4; ++k) *d++ = (uint8_t)((uint64_t)nb >> (8 * k));
+  }
+  const int64_t have = std::min<int64_t>(nb, 4 * (int64_t)n2w);
+  memcpy(d, row, (size_t)have);
+  d += have;
+  for (int64_t k = have; k < nb; ++k) *d++ = 0;
+  *d++ = 'h';
+  *d++ = 3;
+  if (e >= 0 && e < 256) {
+    *d++ = 'K';
+    *d++ = (uint8_t)e;
+  } else {
+    *d++ = 'J';
+    for (int k = 0; k < 4; ++k) *d++ = (uint8_t)((uint32_t)e >> (8 * k));
+  }
+  *d++ = 'u';
+  *d++ = 'b';
+  if (i % 1000 == 999 || i == count - 1) *d++ = 'e';
+  return d;
+}
+
 // Returns the byte count; writes only when out != nullptr and it fits in cap.
 // Elements are sized, prefix-summed and written by `threads` host threads
 // over contiguous element ranges (the bytes do not depend on the split).
@@ -216,26 +273,42 @@ inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, in
   std::vector<int64_t> part(T + 1, 0);  // element range bounds
   for (int t = 0; t <= T; ++t) part[t] = count * t / T;
   std::vector<int64_t> bytes(T, 0);
-  auto sizer = [&](int t) {
-    Writer w{nullptr, 0};
-    for (int64_t i = part[t]; i < part[t + 1]; ++i) emit_elem(w, ct + (size_t)i * n2w, n2w, exps[i], i, count);
-    bytes[t] = w.n;
-  };
-  run_parallel(T, sizer);
+  run_parallel(T, [&](int t) {
+    int64_t b = 0;
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) b += elem_bytes(ct + (size_t)i * n2w, n2w, exps[i], i, count);
+    bytes[t] = b;
+  });
   std::vector<int64_t> off(T + 1, head);
   for (int t = 0; t < T; ++t) off[t + 1] = off[t] + bytes[t];
   const int64_t total = off[T] + 3;
   if (!out || total > cap) return total;
   Writer h{out, cap};
   emit_header(h, shape, ndim);
-  auto writer = [&](int t) {
-    Writer w{out + off[t], bytes[t]};
-    for (int64_t i = part[t]; i < part[t + 1]; ++i) emit_elem(w, ct + (size_t)i * n2w, n2w, exps[i], i, count);
-  };
-  run_parallel(T, writer);
+  run_parallel(T, [&](int t) {
+    uint8_t* d = out + off[t];
+    int64_t i = part[t];
+    if (i == 0 && i < part[t + 1]) {  // the first element memoises the class and keys
+      Writer w{d, bytes[t]};
+      emit_elem(w, ct, n2w, exps[0], 0, count);
+      d += w.n;
+      ++i;
+    }
+    for (; i < part[t + 1]; ++i) d = write_elem(d, ct + (size_t)i * n2w, n2w, exps[i], i, count);
+  });
   Writer f{out + off[T], 3};
   emit_footer(f);
   return total;
+}
+
+// The same bytes written one put() at a time (the specification the fast
+// encoder is checked against in tests/native/host_fuzz.cpp).
+inline int64_t encode_reference(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,
+                                int ndim, uint8_t* out, int64_t cap) {
+  Writer w{out, out ? cap : 0};
+  emit_header(w, shape, ndim);
+  for (int64_t i = 0; i < count; ++i) emit_elem(w, ct + (size_t)i * n2w, n2w, exps[i], i, count);
+  emit_footer(w);
+  return w.n;
 }
 
 // ------------------------------------------------------------------ decoder

@@ -91,7 +91,7 @@ def encrypt_floats_words(ctx, xs, precision, max_exponent, obfuscation, num_core
     x = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1)
     n = x.shape[0]
     n2w = n2w_of(ctx)
-    ct = np.empty((n, n2w), dtype=np.uint32)
+    ct = nat.empty((n, n2w), np.uint32)
     ex = np.empty(n, dtype=np.int32)
     st = np.empty(n, dtype=np.int32)
     if n == 0:
@@ -114,7 +114,7 @@ def encrypt_encoded_words(ctx, mw, obfuscation, num_cores=-1):
     """encrypt already-encoded integers m (0 <= m < n, nw words each)."""
     mw = _u32(mw)
     n = mw.shape[0]
-    ct = np.empty((n, n2w_of(ctx)), dtype=np.uint32)
+    ct = nat.empty((n, n2w_of(ctx)), np.uint32)
     if n == 0:
         return ct
     if obfuscation:
@@ -180,7 +180,7 @@ def add_words(ctx, aw, ea, bw, eb, num_cores=-1):
     aw, bw = _u32(aw), _u32(bw)
     ea, eb = _i32(ea), _i32(eb)
     n = aw.shape[0]
-    out = np.empty_like(aw)
+    out = nat.empty(aw.shape, np.uint32)
     eo = np.empty(n, dtype=np.int32)
     if n == 0:
         return out, eo
@@ -198,7 +198,7 @@ def powmod_words(ctx, cw, kw_, kbits, invert_first=False, num_cores=-1):
     cw = _u32(cw)
     kw_ = _u32(kw_)
     n = cw.shape[0]
-    out = np.empty_like(cw)
+    out = nat.empty(cw.shape, np.uint32)
     if n == 0:
         return out
     kwords = kw_.shape[1]

@@ -40,9 +40,11 @@ def encode_words(ct, exps, shape):
         nat.check(rc, "wire encode")
     # written straight into the bytes object handed back (no staging copy of
     # the ~0.5 KB/ciphertext payload); nothing else references it yet
-    out = bytes(need.value)
-    rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), ctypes.cast(out, ctypes.c_void_p),
-                           need.value, ctypes.byref(need))
+    out = bytes(need.value)  # > 100 bytes (header): never a shared singleton
+    ptr = ctypes.cast(out, ctypes.c_void_p)
+    nat.advise_huge(ptr.value, need.value)
+    rc = L.xhe_wire_encode(_vp(ct), _vp(ex), count, n2w, _vp(shp), len(shape), ptr, need.value,
+                           ctypes.byref(need))
     nat.check(rc, "wire encode")
     return out
 
@@ -85,7 +87,7 @@ def _decode(data, n2w):
     shape = np.zeros(8, dtype=np.int64)
     cap = max(1, len(data) // (4 * n2w) + 16)
     for _ in range(2):
-        ct = np.empty((cap, n2w), dtype=np.uint32)
+        ct = nat.empty((cap, n2w), np.uint32)
         ex = np.empty(cap, dtype=np.int32)
         rc = L.xhe_wire_decode(_vp(buf), len(data), n2w, _vp(ct), _vp(ex), cap, ctypes.byref(count), _vp(shape),
                                ctypes.byref(ndim))
