@@ -82,13 +82,12 @@ def cpu_baseline(bits, seconds, cores):
                       f"{cores} worker processes x ~{seconds:.0f}s, pure-Python pow (oracle/bench_cpu.py)"}
 
 
-TABLE_ROW_BYTES = {2048: 304, 3072: 448, 4096: 608, 8192: 1216}  # S4 words x 4 (xhe.hip Shape<K>::MP2::S4)
+TABLE_ROW_BYTES = {2048: 256, 3072: 384, 4096: 512, 8192: 1024}  # packed rows: K/32 words x 4 (xhe.hip Shape<K>::RW)
 
 
 def table_bytes(bits, win):
     """Device bytes of the two fixed-base tables (xhe_key_create, include/xhe.h):
-    ceil(rand_bits/win) windows x 2^win rows x S4 words per prime, S4 the
-    radix-2^28 limb count of P^2 rounded up to 4."""
+    ceil(rand_bits/win) windows x 2^win packed rows of K/32 words per prime."""
     rand_bits = bits // 2
     return 2 * -(-rand_bits // win) * (1 << win) * TABLE_ROW_BYTES[bits]
 

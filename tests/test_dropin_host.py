@@ -114,7 +114,7 @@ def test_table_window_policy(monkeypatch):
     priv.note_encrypt_volume(2_000_000)
     assert priv.device_key().win_bits == 20
     priv.note_encrypt_volume(100_000_000)
-    free["b"] = 100 << 30  # 2 x 59.9 GB + 32 GiB margin does not fit next to the win-20 tables' 33 GB
+    free["b"] = 90 << 30  # 2 x 50.4 GB + 32 GiB margin does not fit next to the win-20 tables' 27.9 GB
     assert priv.device_key().win_bits == 20
     free["b"] = 200 << 30
     assert priv.device_key().win_bits == 22

@@ -121,7 +121,7 @@ def test_djn_encrypt_both_shapes():
                 assert big[i] == O.encrypt_m(ok, ms[i], rs[i])
 
 
-@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+@pytest.mark.parametrize("fx", ["paillier_2048_djn.json", "paillier_3072_djn.json", "paillier_4096_djn.json"])
 def test_private_nodjn_encrypt_closed_form(fx):
     """Private-key non-DJN encryption (r^ep mod p^2, r^eq mod q^2, CRT;
     paillier.py:214-230) equals the closed form (1 + n m) r^n mod n^2 —
@@ -140,3 +140,22 @@ def test_private_nodjn_encrypt_closed_form(fx):
     for i in list(range(4)) + [count - 1]:
         assert ct[i] == (1 + n * ms[i]) * pow(rs[i], n, n2) % n2, i
     assert nat.words_to_ints(dk.decrypt_words(nat.ints_to_words(ct, dk.n2w))) == ms
+
+
+@pytest.mark.parametrize("fx", ["paillier_2048_djn.json", "paillier_3072_djn.json", "paillier_4096_djn.json"])
+def test_public_nodjn_encrypt_closed_form(fx):
+    """Public-key encryption without h^n (the remote party's mode,
+    context.py:152-168; paillier.py:228-230): (1 + n m) r^n mod n^2 with the
+    exponent n walked by the wave-uniform sliding window."""
+    from xfl_amd import _native as nat
+    k = load_fixture(fx)["key"]
+    n = hx(k["n"])
+    n2 = n * n
+    dk = nat.DeviceKey(int(fx.split("_")[1]), n, None, None, None, device=0)
+    rng = random.Random(12)
+    count = 1500
+    ms = [rng.randrange(n) for _ in range(count)]
+    rs = [rng.randrange(1, n) for _ in range(count)]
+    ct = nat.words_to_ints(dk.encrypt_words(nat.ints_to_words(ms, dk.nw), nat.ints_to_words(rs, dk.rand_words)))
+    for i in list(range(4)) + [count // 2, count - 1]:
+        assert ct[i] == (1 + n * ms[i]) * pow(rs[i], n, n2) % n2, i

@@ -187,12 +187,12 @@ def ptr(a):
     return a.ctypes.data_as(_u32p)
 
 
-TABLE_ROW_WORDS = {2048: 76, 3072: 112, 4096: 152, 8192: 304}  # xhe.hip Shape<K>::MP2::S4
+TABLE_ROW_WORDS = {2048: 64, 3072: 96, 4096: 128, 8192: 256}  # packed rows: xhe.hip Shape<K>::RW = K/32
 
 
 def table_bytes(key_bits, win_bits):
     """Device bytes of a DJN private key's two fixed-base tables: ceil(rand_bits
-    / win) windows x 2^win rows x S4 words per prime (rand_bits = K/2)."""
+    / win) windows x 2^win packed rows of K/32 words per prime (rand_bits = K/2)."""
     if not win_bits:
         return 0
     return 2 * -(-(key_bits // 2) // win_bits) * (1 << win_bits) * TABLE_ROW_WORDS[key_bits] * 4

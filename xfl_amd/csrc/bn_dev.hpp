@@ -48,7 +48,6 @@ namespace xhe {
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif
-
 // d = a*b + c with one v_mad_u64_u32. Inline asm keeps a and b 32-bit: the
 // C form (uint64_t)a*b + c makes the compiler hold every limb as a
 // zero-extended 64-bit register pair, doubling the resident operand.
@@ -784,7 +783,7 @@ struct Mont {
 #pragma unroll
     for (int j = 0; j < L; ++j) ws[(size_t)(S + g * L + j) * stride] = hi[j];
     wave_sync_mem_();
-    pack_words_<W, TPI>(ws, stride, 2 * S, out, nwords);
+    if (out) pack_words_<W, TPI>(ws, stride, 2 * S, out, nwords);
   }
 
   // ---------------------------------------------------------------- I/O

@@ -36,6 +36,7 @@ struct HipError : std::runtime_error {
 // ------------------------------------------------------------------ shapes
 // Limb shapes per key size: MP2 for residues mod p^2/q^2, MP for mod p/q.
 struct Shape2048 {
+  static constexpr int K = 2048, RW = K / 32, RW2 = K / 16;  // packed table row words mod p^2 / n^2
   using MP2 = Mont<74, 28, 1>;
   using MP2L = Mont<76, 28, 4>;   // low-latency (small-batch) decrypt shape
   using MP2X = Mont<80, 28, 16>;  // lowest latency: one 16-lane DPP row per residue (tiny batches)
@@ -44,6 +45,7 @@ struct Shape2048 {
   using MN2X = Mont<160, 27, 16>;  // n^2 ops on small batches: one 16-lane DPP row per residue
 };
 struct Shape3072 {
+  static constexpr int K = 3072, RW = K / 32, RW2 = K / 16;  // packed table row words mod p^2 / n^2
   using MP2 = Mont<110, 28, 2>;
   using MP2L = Mont<112, 28, 4>;
   using MP2X = Mont<112, 28, 16>;
@@ -58,6 +60,7 @@ struct Shape3072 {
 // in both the batch and the small-batch shapes; the mod-p limbs share W with
 // p^2 so k_dec_fin reads k_dec_pow's rows unchanged.
 struct Shape4096 {
+  static constexpr int K = 4096, RW = K / 32, RW2 = K / 16;  // packed table row words mod p^2 / n^2
   using MP2 = Mont<152, 27, 4>;
   using MP2L = Mont<152, 27, 4>;
   using MP2X = Mont<160, 27, 16>;
@@ -70,6 +73,7 @@ struct Shape4096 {
 // lanes; n^2 (16384 bits) needs 26-bit limbs for the lazy accumulator
 // ((2S+2) 2^52 < 2^64 at S = 640), 40 per lane of a 16-lane row.
 struct Shape8192 {
+  static constexpr int K = 8192, RW = K / 32, RW2 = K / 16;  // packed table row words mod p^2 / n^2
   using MP2 = Mont<304, 27, 16>;
   using MP2L = Mont<304, 27, 16>;
   using MP2X = Mont<304, 27, 16>;
@@ -171,54 +175,60 @@ struct DevGuard {
   }
 };
 
-template <class MP2>
-void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_ws,
-                    hipStream_t s);
+template <class MP2, int RW>
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
+                    uint32_t* d_ws, hipStream_t s);
 
 // Tables of one modulus, or of p^2 and q^2 concurrently on two streams.
-template <class MP2>
+template <class MP2, int RW>
 void build_tables_sync(xhe_key* k, const ModDev* md, const uint32_t* const* d_hM, uint32_t* const* d_tab, int count) {
   hipStream_t st[2] = {nullptr, nullptr};
   uint32_t* ws[2] = {nullptr, nullptr};
+  uint32_t* chain[2] = {nullptr, nullptr};
+  const int win = k->kd.win;
+  const size_t chain_words =
+      (size_t)k->kd.nwin * (((size_t)1 << (win / 2)) + ((size_t)1 << (win - win / 2))) * MP2::S4;
   for (int i = 0; i < count; ++i) {
     HIPCHK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
     HIPCHK(hipMalloc(&ws[i], MP2::S4 * sizeof(uint32_t) * 4));
-    build_tables_m<MP2>(k, md[i], d_hM[i], d_tab[i], ws[i], st[i]);
+    HIPCHK(hipMalloc(&chain[i], chain_words * sizeof(uint32_t)));
+    build_tables_m<MP2, RW>(k, md[i], d_hM[i], d_tab[i], chain[i], ws[i], st[i]);
   }
   for (int i = 0; i < count; ++i) {
     HIPCHK(hipStreamSynchronize(st[i]));
     HIPCHK(hipFree(ws[i]));
+    HIPCHK(hipFree(chain[i]));
     HIPCHK(hipStreamDestroy(st[i]));
   }
 }
 
-// Fixed-base table build, enqueued on `s` (no synchronisation; d_ws must
-// stay alive until s has drained): bases tab[w][1] = h^(2^(win w)) by one
-// squaring chain, every window's low and high chains by doubling levels
-// (k_tab_level: log2 depth instead of 2^(win/2)), then every remaining row
-// as one product of a high and a low entry.
-template <class MP2>
-void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_ws,
-                    hipStream_t s) {
+// Fixed-base table build, enqueued on `s` (no synchronisation; d_ws and
+// d_chain must stay alive until s has drained): bases (low entry 1 of every
+// window) = h^(2^(win w)) by one squaring chain, every window's low and high
+// chains by doubling levels (k_tab_level: log2 depth instead of 2^(win/2)),
+// then every packed row as one product of a high and a low entry.
+template <class MP2, int RW>
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
+                    uint32_t* d_ws, hipStream_t s) {
   const int win = k->kd.win, nwin = k->kd.nwin, half = win / 2;
-  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, win, nwin, d_tab, d_ws);
+  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, win, nwin, d_chain, d_ws);
   HIPCHK(hipGetLastError());
   auto blocks = [&](int64_t groups) { return dim3((unsigned)std::max<int64_t>(1, (groups * MP2::TPI + 255) / 256)); };
-  hipLaunchKernelGGL(k_tab_one<MP2>, blocks(nwin), dim3(256), 0, s, md, win, nwin, d_tab);
+  hipLaunchKernelGGL(k_tab_one<MP2>, blocks(nwin), dim3(256), 0, s, md, win, nwin, d_chain);
   HIPCHK(hipGetLastError());
   const int lim_lo = (1 << half) + 1, lim_hi = 1 << (win - half);
   for (int t = 0; (1 << t) < lim_lo - 1; ++t) {
     hipLaunchKernelGGL(k_tab_level<MP2>, blocks((int64_t)nwin << t), dim3(256), 0, s, md, md.N, win, nwin, t, 0,
-                       lim_lo, d_tab);
+                       lim_lo, d_chain);
     HIPCHK(hipGetLastError());
   }
   for (int t = 0; (1 << t) < lim_hi - 1; ++t) {
     hipLaunchKernelGGL(k_tab_level<MP2>, blocks((int64_t)nwin << t), dim3(256), 0, s, md, md.N, win, nwin, t, half,
-                       lim_hi, d_tab);
+                       lim_hi, d_chain);
     HIPCHK(hipGetLastError());
   }
   int64_t rows = (int64_t)nwin << win;
-  hipLaunchKernelGGL(k_tab_combine<MP2>, blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_tab);
+  hipLaunchKernelGGL((k_tab_combine<MP2, RW>), blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_chain, d_tab);
   HIPCHK(hipGetLastError());
 }
 
@@ -402,26 +412,32 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       kd.win = win;
       kd.nwin = (k->rand_bits + win - 1) / win;
       size_t rows = (size_t)kd.nwin << win;
-      size_t tab_words = rows * k->mp2.S4();
+      size_t tab_words = rows * (size_t)(K / 32);  // packed rows: Shape::RW = K/32 words (p^2 < 2^K)
       HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
       kd.tab_p2 = k->d_tab;
       kd.tab_q2 = k->d_tab + tab_words;
       const ModDev mds[2] = {kd.p2, kd.q2};
       const uint32_t* hms[2] = {B + o.hM_p2, B + o.hM_q2};
       uint32_t* tabs[2] = {k->d_tab, k->d_tab + tab_words};
-      with_shape(K, [&](auto sh) { build_tables_sync<typename decltype(sh)::MP2>(k, mds, hms, tabs, 2); });
+      with_shape(K, [&](auto sh) {
+        using Sh = decltype(sh);
+        build_tables_sync<typename Sh::MP2, Sh::RW>(k, mds, hms, tabs, 2);
+      });
     }
   }
   if (!k->priv && k->djn) {
     kd.win = win;
     kd.nwin = (k->rand_bits + win - 1) / win;
     size_t rows = (size_t)kd.nwin << win;
-    size_t tab_words = rows * k->mn2.S4();
+    size_t tab_words = rows * (size_t)(K / 16);  // packed rows: Shape::RW2 = n2w words
     HIPCHK(hipMalloc(&k->d_tab, tab_words * sizeof(uint32_t)));
     kd.tab_n2 = k->d_tab;
     const uint32_t* hm = B + o_hMn2;
     uint32_t* tab = k->d_tab;
-    with_shape(K, [&](auto sh) { build_tables_sync<typename decltype(sh)::MN2>(k, &kd.n2, &hm, &tab, 1); });
+    with_shape(K, [&](auto sh) {
+      using Sh = decltype(sh);
+      build_tables_sync<typename Sh::MN2, Sh::RW2>(k, &kd.n2, &hm, &tab, 1);
+    });
   }
 }
 
@@ -480,6 +496,18 @@ bool enc_row(int64_t count) {
   return pin >= 0 ? pin == 16 : count <= kEncRowMax;
 }
 
+// CRT of the two prime rows in ws into ciphertext words (k_crt_enc; the
+// one-lane shape writes through LDS so its stores are whole lines)
+template <class MP2>
+void crt_enc_launch(const xhe_key* k, int64_t n, uint32_t* ws, uint32_t* ct, hipStream_t s) {
+  const int blocks = (int)((n * MP2::TPI + 255) / 256);
+  if constexpr (MP2::TPI == 1)
+    hipLaunchKernelGGL(k_crt_enc_t<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws, ct);
+  else
+    hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws, ct);
+  HIPCHK(hipGetLastError());
+}
+
 template <class Sh>
 void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -492,26 +520,24 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     if (enc_row(n)) {
       // small batch: one 16-lane DPP row per residue (latency-bound regime)
       using MX = typename Sh::MP2X;
-      hipLaunchKernelGGL((k_djn_pow_x<MX, MP2::S4>), dim3((unsigned)((n * MX::TPI + 255) / 256), 2), dim3(256), 0, s,
+      hipLaunchKernelGGL((k_djn_pow_x<MX, MP2::S4, Sh::RW>), dim3((unsigned)((n * MX::TPI + 255) / 256), 2), dim3(256), 0, s,
                          k->kd, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, ws);
       HIPCHK(hipGetLastError());
     } else {
       ProfScope ps("k_djn_pow", s);
 #if XHE_LDS_ROWS
       if constexpr (MP2::TPI == 1) {
-        hipLaunchKernelGGL(k_djn_pow_lds<MP2>, dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
+        hipLaunchKernelGGL((k_djn_pow_lds<MP2, Sh::RW>), dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
                            k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
                            k->rand_words, n, ws);
       } else
 #endif
-      hipLaunchKernelGGL(k_djn_pow<MP2>, dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
+      hipLaunchKernelGGL((k_djn_pow<MP2, Sh::RW>), dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p2.N, k->kd.q2.N,
                          m + (size_t)off * k->nw,
                          r + (size_t)off * k->rand_words, k->rand_words, n, ws);
       HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws,
-                       ct + (size_t)off * k->n2w);
-    HIPCHK(hipGetLastError());
+    crt_enc_launch<MP2>(k, n, ws, ct + (size_t)off * k->n2w, s);
   }
   HIPCHK(hipFreeAsync(ws, s));
 }
@@ -533,7 +559,7 @@ void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MN2::TPI + 255) / 256);
     ProfScope ps("k_djn_pub", s);
-    hipLaunchKernelGGL(k_djn_pub<MN2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.n2.N, m + (size_t)off * k->nw,
+    hipLaunchKernelGGL((k_djn_pub<MN2, Sh::RW2>), dim3(blocks), dim3(256), 0, s, k->kd, k->kd.n2.N, m + (size_t)off * k->nw,
                        r + (size_t)off * k->rand_words, k->rand_words, n, ws, ct + (size_t)off * k->n2w);
     HIPCHK(hipGetLastError());
   }
@@ -565,10 +591,7 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
                            m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, rows, ws);
         HIPCHK(hipGetLastError());
       }
-      int blocks = (int)((n * MP2::TPI + 255) / 256);
-      hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, rows,
-                         ct + (size_t)off * k->n2w);
-      HIPCHK(hipGetLastError());
+      crt_enc_launch<MP2>(k, n, rows, ct + (size_t)off * k->n2w, s);
     }
     HIPCHK(hipFreeAsync(ws, s));
     HIPCHK(hipFreeAsync(rows, s));
@@ -978,9 +1001,18 @@ void rand_impl(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_
   memcpy(ck.k, seed32, 32);
   ck.nonce0 = (uint32_t)nonce;
   ck.nonce1 = (uint32_t)(nonce >> 32);
-  int blocks = (int)((count + 255) / 256);
-  hipLaunchKernelGGL(k_rand_below, dim3(blocks), dim3(256), 0, s, ck, base, count, key->rand_words, key->rand_bits,
-                     key->djn ? (const uint32_t*)nullptr : key->kd.n_words, rand_dev, status_dev);
+  if (key->djn) {
+    // no rejection: one thread per ChaCha20 block, the element's lanes adjacent
+    int tpe = 1;
+    while (tpe < (key->rand_words + 15) / 16) tpe <<= 1;
+    int blocks = (int)((count * tpe + 255) / 256);
+    hipLaunchKernelGGL(k_rand_djn, dim3(blocks), dim3(256), 0, s, ck, base, count, key->rand_words, key->rand_bits,
+                       tpe, rand_dev, status_dev);
+  } else {
+    int blocks = (int)((count + 255) / 256);
+    hipLaunchKernelGGL(k_rand_below, dim3(blocks), dim3(256), 0, s, ck, base, count, key->rand_words,
+                       key->rand_bits, key->kd.n_words, rand_dev, status_dev);
+  }
   HIPCHK(hipGetLastError());
 }
 }  // namespace
@@ -1071,7 +1103,7 @@ int xhe_encode_f64(const xhe_key* key, const double* x_dev, int64_t count, int p
     int mode = precision < 0 ? 0 : 1;
     // -ceil(log2(10) * precision) (encoder.py:39), computed exactly as Python does in float64
     int e0 = precision < 0 ? 0 : -(int)std::ceil(std::log2(10.0) * (double)precision);
-    int blocks = (int)((count + 255) / 256);
+    int blocks = (int)((count * (key->nw / 4) + 255) / 256);  // one thread per 16-byte quad of m
     hipLaunchKernelGGL(k_encode_f64, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x_dev, count, mode, e0,
                        has_max, max_exponent, key->kd.n_words, key->nw, m_dev, exp_dev, status_dev);
     HIPCHK(hipGetLastError());

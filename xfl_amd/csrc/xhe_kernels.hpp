@@ -76,18 +76,20 @@ struct KeyDev {
 // status codes per element (mirrors the exceptions the reference raises)
 enum : int32_t { ST_OK = 0, ST_OVERFLOW = 1, ST_VALUE = 2 };
 
-// One element per thread: float64 x -> m = round_half_even(x * 2^-e) mod n,
-// e from `mode` (0: frexp(x)-53, i.e. precision None; 1: fixed e0) clamped by
-// max_exponent when has_max. Writes nw words of m and the exponent.
-__global__ void k_encode_f64(const double* __restrict__ x, int64_t count, int mode, int e0, int has_max,
-                             int max_exp, const uint32_t* __restrict__ n_words, int nw,
-                             uint32_t* __restrict__ m_out, int32_t* __restrict__ e_out,
-                             int32_t* __restrict__ status) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  double v = x[i];
+// y = round_half_even(x * 2^-e) as |y| = (v0 + v1 2^32 + v2 2^64) 2^(32 w),
+// its sign, the exponent e (mode 0: frexp(x) - 53, i.e. precision None;
+// mode 1: fixed e0; clamped by max_exponent when has_max) and the status the
+// reference's encode raises for x (encoder.py:29-54).
+struct EncVal {
+  int32_t st, e;
+  int neg, w;
+  uint32_t v0, v1, v2;
+};
+
+XHE_DEV EncVal encode_value(double v, int mode, int e0, int has_max, int max_exp) {
+  EncVal r{ST_OK, 0, 0, 0, 0u, 0u, 0u};
   uint64_t bits = __double_as_longlong(v);
-  int neg = (int)(bits >> 63);
+  r.neg = (int)(bits >> 63);
   int bexp = (int)((bits >> 52) & 0x7FF);
   uint64_t frac = bits & ((1ull << 52) - 1);
   int e;
@@ -95,62 +97,101 @@ __global__ void k_encode_f64(const double* __restrict__ x, int64_t count, int mo
     // math.frexp(x)[1] - 53; frexp(0) = (0, 0); frexp(inf/nan) = (x, 0)
     int fe;
     if (bexp == 0x7FF || (bexp == 0 && frac == 0)) fe = 0;
-    else if (bexp == 0) fe = -1022 - (__clzll(frac) - 12) ;  // subnormal: frexp exponent
+    else if (bexp == 0) fe = -1022 - (__clzll(frac) - 12);  // subnormal: frexp exponent
     else fe = bexp - 1022;
     e = fe - 53;
   } else {
     e = e0;
   }
   if (has_max && max_exp < e) e = max_exp;
-  uint32_t* mo = m_out + (size_t)i * nw;
-  e_out[i] = e;
-  int32_t st = ST_OK;
+  r.e = e;
   // x * (1 << -e): negative shift -> ValueError; shift >= 1024 -> int->float OverflowError
-  if (-e < 0) st = ST_VALUE;
-  else if (-e >= 1024) st = ST_OVERFLOW;
-  else if (bexp == 0x7FF) st = frac ? ST_VALUE : ST_OVERFLOW;  // round(nan) / round(inf)
+  if (-e < 0) r.st = ST_VALUE;
+  else if (-e >= 1024) r.st = ST_OVERFLOW;
+  else if (bexp == 0x7FF) r.st = frac ? ST_VALUE : ST_OVERFLOW;  // round(nan) / round(inf)
   // M * 2^E exact decomposition
   uint64_t M;
   int E;
   if (bexp == 0) { M = frac; E = -1074; } else { M = frac | (1ull << 52); E = bexp - 1075; }
   int sh = E - e;  // y = M * 2^sh
   // float product overflow (|y| >= 2^1024) -> inf -> round(inf) OverflowError
-  if (st == ST_OK && M != 0) {
+  if (r.st == ST_OK && M != 0) {
     int top = 64 - __clzll(M) + sh;  // y < 2^top
-    if (top > 1024) st = ST_OVERFLOW;
+    if (top > 1024) r.st = ST_OVERFLOW;
   }
-  for (int k = 0; k < nw; ++k) mo[k] = 0;
-  status[i] = st;
-  if (st != ST_OK || M == 0) return;
-  // integer q = round_half_even(M * 2^sh)
+  if (r.st != ST_OK || M == 0) return r;
   if (sh >= 0) {
-    int w = sh >> 5, b = sh & 31;
+    int b = sh & 31;
     uint64_t lo = M << b;                                 // bits [w*32, w*32+64)
-    uint32_t hi = b ? (uint32_t)(M >> (64 - b)) : 0u;     // bits [w*32+64, +96)
-    if (w < nw) mo[w] = (uint32_t)lo;
-    if (w + 1 < nw) mo[w + 1] = (uint32_t)(lo >> 32);
-    if (w + 2 < nw) mo[w + 2] = hi;
+    r.w = sh >> 5;
+    r.v0 = (uint32_t)lo;
+    r.v1 = (uint32_t)(lo >> 32);
+    r.v2 = b ? (uint32_t)(M >> (64 - b)) : 0u;            // bits [w*32+64, +96)
   } else {
-    int r = -sh;
+    int rr = -sh;
     uint64_t q, rem, half;
-    if (r >= 64) { q = 0; rem = M; half = (r == 64) ? (1ull << 63) : ~0ull; if (r > 64) { q = 0; rem = 0; } }
-    else { q = M >> r; rem = M & ((1ull << r) - 1); half = 1ull << (r - 1); }
-    if (r <= 64 && (rem > half || (rem == half && (q & 1)))) q += 1;
-    mo[0] = (uint32_t)q;
-    mo[1] = (uint32_t)(q >> 32);
+    if (rr >= 64) { q = 0; rem = M; half = (rr == 64) ? (1ull << 63) : ~0ull; if (rr > 64) { q = 0; rem = 0; } }
+    else { q = M >> rr; rem = M & ((1ull << rr) - 1); half = 1ull << (rr - 1); }
+    if (rr <= 64 && (rem > half || (rem == half && (q & 1)))) q += 1;
+    r.v0 = (uint32_t)q;
+    r.v1 = (uint32_t)(q >> 32);
   }
-  if (neg) {
-    // m = n - |y| (|y| < 2^1077 < n for K >= 2048), or 0 when y == 0
-    bool zero = true;
-    for (int k = 0; k < nw; ++k) zero &= mo[k] == 0;
-    if (!zero) {
-      int64_t br = 0;
-      for (int k = 0; k < nw; ++k) {
-        int64_t d = (int64_t)n_words[k] - (int64_t)mo[k] - br;
-        br = d < 0;
-        mo[k] = (uint32_t)(d + (br << 32));
+  return r;
+}
+
+XHE_DEV uint32_t enc_word(const EncVal& y, int k) {
+  const int d = k - y.w;
+  return d == 0 ? y.v0 : d == 1 ? y.v1 : d == 2 ? y.v2 : 0u;
+}
+
+// float64 x -> m = y mod n (n - |y| for negative y, |y| < 2^1077 < n for
+// K >= 2048), exponent and status per element. One thread per 16-byte quad
+// of m (nw/4 threads per element, nw a multiple of 4): a wave writes whole
+// consecutive rows, so the stores are coalesced.
+__global__ void k_encode_f64(const double* __restrict__ x, int64_t count, int mode, int e0, int has_max,
+                             int max_exp, const uint32_t* __restrict__ n_words, int nw,
+                             uint32_t* __restrict__ m_out, int32_t* __restrict__ e_out,
+                             int32_t* __restrict__ status) {
+  const int nq = nw >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t / nq;
+  if (i >= count) return;
+  const int q = (int)(t - i * nq);
+  const EncVal y = encode_value(x[i], mode, e0, has_max, max_exp);
+  if (q == 0) {
+    e_out[i] = y.e;
+    status[i] = y.st;
+  }
+  uint32_t o[4] = {0u, 0u, 0u, 0u};
+  const bool zero = y.st != ST_OK || (y.v0 | y.v1 | y.v2) == 0u;
+  if (!zero) {
+    if (!y.neg) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = enc_word(y, 4 * q + k);
+    } else {
+      // n - |y|: the borrow into word 4q comes from words [w, 4q) only
+      // (|y| is zero below w), and propagates past w + 2 only through zero words of n
+      uint32_t br = 0;
+      const int kend = min(4 * q, y.w + 3);
+      for (int k = y.w; k < kend; ++k) {  // at most the 3 words of |y|
+        const uint32_t nk = n_words[k], yk = enc_word(y, k);
+        br = (nk < yk || (nk == yk && br)) ? 1u : 0u;
+      }
+      for (int k = y.w + 3; k < 4 * q && br; ++k) br = n_words[k] == 0u ? 1u : 0u;  // through zero words only
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t nk = n_words[4 * q + k], yk = enc_word(y, 4 * q + k);
+        o[k] = nk - yk - br;
+        br = (nk < yk || (nk == yk && br)) ? 1u : 0u;
       }
     }
+  }
+  uint32_t* dst = m_out + (size_t)i * nw + 4 * q;
+  if ((reinterpret_cast<uintptr_t>(m_out) & 15u) == 0u) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {  // a caller's buffer that is not 16-byte aligned
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = o[k];
   }
 }
 
@@ -184,16 +225,10 @@ struct ChaChaKey { uint32_t k[8]; uint32_t nonce0, nonce1; };
 // else in [1, bound) by rejection (non-DJN r in [1, n), paillier.py:215).
 // `words` 32-bit words per element; element i (= base + thread) uses counter
 // block (i * 64 + attempt) * blocks_per_draw.
-__global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
-                             const uint32_t* __restrict__ bound, uint32_t* __restrict__ out,
-                             int32_t* __restrict__ status) {
-  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= count) return;
-  uint32_t* o = out + (size_t)li * words;
-  status = status ? status + li : nullptr;
-  const int64_t i = base + li;  // stream position: independent of how a batch is split into launches
+XHE_DEV void rand_elem(const ChaChaKey& ck, int64_t i, int words, int bits, const uint32_t* __restrict__ bound,
+                       uint32_t* __restrict__ o, int32_t* __restrict__ status, int first_attempt) {
   const int blocks = (words + 15) / 16;
-  for (int attempt = 0; attempt < 64; ++attempt) {
+  for (int attempt = first_attempt; attempt < 64; ++attempt) {
     for (int b = 0; b < blocks; ++b) {
       uint32_t ks[16];
       chacha20_block(ck.k, ck.nonce0, ck.nonce1, ((uint64_t)i * 64 + attempt) * blocks + b, ks);
@@ -218,24 +253,107 @@ __global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int word
   if (status) *status = ST_VALUE;
 }
 
+__global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
+                             const uint32_t* __restrict__ bound, uint32_t* __restrict__ out,
+                             int32_t* __restrict__ status) {
+  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= count) return;
+  // stream position base + li: independent of how a batch is split into launches
+  rand_elem(ck, base + li, words, bits, bound, out + (size_t)li * words, status ? status + li : nullptr, 0);
+}
+
+// The DJN draw (no upper bound) with one thread per ChaCha20 block: the `tpe`
+// (a power of two >= blocks) adjacent lanes of one wave make one element, and
+// each writes its 64 bytes with 16-byte stores, so a wave writes consecutive
+// rows. The same stream and the same words as k_rand_below: attempt 0 is the
+// draw unless it is zero (probability 2^-bits), which the group's ballot
+// detects and the group's first lane redraws from attempt 1 on.
+__global__ void k_rand_djn(ChaChaKey ck, int64_t base, int64_t count, int words, int bits, int tpe,
+                           uint32_t* __restrict__ out, int32_t* __restrict__ status) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t li = t / tpe;
+  const int b = (int)(t & (tpe - 1));
+  const int blocks = (words + 15) / 16;
+  const bool mine = li < count && b < blocks;  // every lane reaches the ballot
+  uint32_t ks[16];
+  bool nz = false;
+  if (mine) {
+    chacha20_block(ck.k, ck.nonce0, ck.nonce1, (uint64_t)(base + li) * 64 * blocks + b, ks);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = b * 16 + u, lo = 32 * k;
+      if (k >= words || lo >= bits) ks[u] = 0u;
+      else if (bits - lo < 32) ks[u] &= (1u << (bits - lo)) - 1u;
+      nz |= ks[u] != 0u;
+    }
+  }
+  const uint64_t ball = __builtin_amdgcn_ballot_w64(nz);
+  const int lane = (int)(threadIdx.x & 63);
+  const uint64_t gmask = (tpe >= 64 ? ~0ull : ((1ull << tpe) - 1ull)) << (lane & ~(tpe - 1));
+  if (!mine) return;
+  if (ball & gmask) {
+    uint32_t* o = out + (size_t)li * words + 16 * b;
+    const int nwb = min(16, words - 16 * b);
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) == 0u && (words & 3) == 0) {
+      for (int u = 0; u < nwb; u += 4)
+        *reinterpret_cast<uint4*>(o + u) = make_uint4(ks[u], ks[u + 1], ks[u + 2], ks[u + 3]);
+    } else {
+      for (int u = 0; u < nwb; ++u) o[u] = ks[u];
+    }
+    if (b == 0 && status) status[li] = ST_OK;
+  } else if (b == 0) {
+    rand_elem(ck, base + li, words, bits, nullptr, out + (size_t)li * words, status ? status + li : nullptr, 1);
+  }
+}
+
 // ============================================================== encrypt
+// A table row is stored packed (RW = K/32 words mod p^2, K/16 mod n^2; 256
+// bytes at 2048 bits:
+// two whole 128-byte lines) and unpacked to W-bit limbs where it is used.
+// One limb of a packed row.
+template <int W, int PW>
+XHE_DEV uint32_t packed_limb(const uint32_t* p, int l) {
+  const int bit = W * l, k = bit >> 5, sh = bit & 31;
+  const uint32_t lo = k < PW ? p[k] : 0u;
+  const uint32_t hi = k + 1 < PW ? p[k + 1] : 0u;
+  return __builtin_amdgcn_alignbit(hi, lo, sh) & ((1u << W) - 1u);
+}
+// Operand a read from a packed row (limbs beyond the row are zero).
+template <int W, int PW>
+struct ARowPacked {
+  const uint32_t* __restrict__ p;
+  XHE_DEV uint4 load4(int i) const {
+    return make_uint4(packed_limb<W, PW>(p, i), packed_limb<W, PW>(p, i + 1), packed_limb<W, PW>(p, i + 2),
+                      packed_limb<W, PW>(p, i + 3));
+  }
+};
+
+// The packed row a lane just staged into its slot of a quad-major LDS image
+// (word k at slot[(k/4)*256 + k%4]) rewritten in place as S4 limbs (limb i
+// at slot[(i/4)*256 + i%4]). Limb quad L reads only words below 4L + 4 (W <
+// 32), so walking L downwards never overwrites a word still to be read.
+template <class MP2, int PW>
+XHE_DEV void unpack_limbs_lds(uint32_t* slot) {
+  constexpr int W = MP2::W;
+  auto word = [&](int k) -> uint32_t { return k < PW ? slot[(k >> 2) * 256 + (k & 3)] : 0u; };
+#pragma unroll
+  for (int L = MP2::S4 / 4 - 1; L >= 0; --L) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int l = 4 * L + j, bit = W * l, k = bit >> 5, sh = bit & 31;
+      v[j] = l < MP2::S ? (__builtin_amdgcn_alignbit(word(k + 1), word(k), sh) & ((1u << W) - 1u)) : 0u;
+    }
+    *reinterpret_cast<uint4*>(slot + L * 256) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // win-bit digit starting at bit `bit` of a little-endian word array (may
 // straddle two words; bits beyond nwords read as zero)
 XHE_DEV uint32_t digit_at(const uint32_t* w, int nwords, int bit, int win) {
   int k = bit >> 5, sh = bit & 31;
   uint64_t v = (uint64_t)(k < nwords ? w[k] : 0u) | ((uint64_t)(k + 1 < nwords ? w[k + 1] : 0u) << 32);
   return (uint32_t)(v >> sh) & ((1u << win) - 1u);
-}
-
-template <class MP2>
-XHE_DEV void fixed_base_pow(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t* tab, int win, int nwin,
-                            const uint32_t* __restrict__ a_words) {
-  const int rows = 1 << win;
-  for (int w = 0; w < nwin; ++w) {
-    int bit = w * win;
-    uint32_t d = digit_at(a_words, nwin * win / 32 + 1, bit, win);
-    M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -246,7 +364,7 @@ XHE_DEV void fixed_base_pow(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t*
 // at row[i * count + e]); the second half of each row is wide-product scratch.
 // Np2/Nq2: the p^2 / q^2 limb rows passed as separate noalias arguments so
 // the modulus limbs are provably read-only and stay in SGPRs (scalar loads).
-template <class MP2>
+template <class MP2, int RW>
 __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* __restrict__ Np2,
                                                     const uint32_t* __restrict__ Nq2,
                                                     const uint32_t* __restrict__ m_words,
@@ -268,7 +386,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   for (int w = 0; w < key.nwin; ++w) {
     int bit = w * key.win;
     uint32_t d = digit_at(ae, aw, bit, key.win);
-    M.mul(b, ARow{tab + ((size_t)w * rows + d) * MP2::S4});
+    M.mul(b, ARowPacked<MP2::W, RW>{tab + ((size_t)w * rows + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -311,22 +429,13 @@ struct SqLds {
   }
 };
 
-// A table row of RS4 words read by a wider-shape Montgomery product (limbs
-// beyond the row are zero).
-template <int RS4>
-struct ARowZ {
-  const uint32_t* __restrict__ p;
-  XHE_DEV uint4 load4(int i) const {
-    return i < RS4 ? *reinterpret_cast<const uint4*>(p + i) : make_uint4(0u, 0u, 0u, 0u);
-  }
-};
 
 // k_djn_pow for small batches: one 16-lane DPP row per residue (key.p2X/q2X)
 // on the same one-lane tables (rows of RS4 words, Montgomery factor R): with
 // the start value (1 + n m) C R', C = (R'/R)^nwin, the nwin table products
 // leave (1 + n m) h^a R' exactly as the one-lane kernel leaves (1 + n m) h^a R.
 // Output rows as k_djn_pow (RS4 limbs, stride count) for k_crt_enc.
-template <class MX, int RS4>
+template <class MX, int RS4, int RW>
 __global__ void __launch_bounds__(256, 2) k_djn_pow_x(KeyDev key, const uint32_t* __restrict__ m_words,
                                                       const uint32_t* __restrict__ a_words, int aw, int64_t count,
                                                       uint32_t* __restrict__ ws) {
@@ -346,7 +455,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow_x(KeyDev key, const uint32_t
   const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
     uint32_t d = digit_at(ae, aw, w * key.win, key.win);
-    M.mul(b, ARowZ<RS4>{tab + ((size_t)w * rows + d) * RS4});
+    M.mul(b, ARowPacked<MX::W, RW>{tab + ((size_t)w * rows + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -373,7 +482,7 @@ struct ALdsQ {
 // (1 + n m) enters once, in plain form, as the last multiplier, so the
 // conversion out of Montgomery form is that same product: nwin + 1 products
 // instead of nwin + 2 ((1 + n m) R first, a final multiply by 1).
-template <class MP2>
+template <class MP2, int RW>
 XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, const ModDev& md,
                            const uint32_t* tab, const uint32_t* nR2, const uint32_t* nR,
                            const uint32_t* __restrict__ m_words, const uint32_t* __restrict__ a_words, int aw,
@@ -386,12 +495,13 @@ XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, c
   const uint32_t* ae = a_words + (size_t)e * aw;
   const int rows = 1 << key.win;
   auto stage = [&](int w) {
-    uint32_t d = digit_at(ae, aw, w * key.win, key.win);
-    const uint32_t* row = tab + ((size_t)w * rows + d) * MP2::S4;
+    const uint32_t d = digit_at(ae, aw, w * key.win, key.win);
+    const uint32_t* row = tab + ((size_t)w * rows + d) * RW;
 #pragma unroll
-    for (int k = 0; k < NQ; ++k)
+    for (int k = 0; k < RW / 4; ++k)
       __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unpack_limbs_lds<MP2, RW>(img + (threadIdx.x & 63) * 4);
   };
 #if XHE_DJN_FOLD
   (void)nR2;
@@ -429,7 +539,7 @@ XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, c
   M.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
 
-template <class MP2>
+template <class MP2, int RW>
 __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32_t* __restrict__ Np2,
                                                         const uint32_t* __restrict__ Nq2,
                                                         const uint32_t* __restrict__ m_words,
@@ -438,10 +548,10 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
   static_assert(MP2::TPI == 1, "LDS row staging is per lane");
   __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= count) return;
   const int prime = blockIdx.y;
   uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
-  djn_prime_lds<MP2>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
+  if (e >= count) return;
+  djn_prime_lds<MP2, RW>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
                      prime ? key.nR2_q2 : key.nR2_p2, prime ? key.nR_q2 : key.nR_p2, m_words, a_words, aw, count, e,
                      prime, img, img + (threadIdx.x & 63) * 4, ws);
 }
@@ -449,6 +559,8 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
 #endif
 
 // c = c_q + q^2 ((c_p + 4p^2 - c_q) (q^2)^-1 mod p^2) for element e (utils.py:38-43)
+// out == nullptr: the 2S result limbs are left in element e's q row of ws
+// (interleaved, limb i at rq[i * count]) for the caller to pack.
 template <class MP2>
 XHE_DEV void crt_enc_elem(const KeyDev& key, const uint32_t* __restrict__ Np2, int64_t count, int64_t e,
                           uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
@@ -462,7 +574,7 @@ XHE_DEV void crt_enc_elem(const KeyDev& key, const uint32_t* __restrict__ Np2, i
   M.add_sub_rows(b, key.p2x4_lim, rq, st);
   M.mul(b, ARow{key.q2invR_p2});
   M.reduce_once(b);
-  M.wide_mul_add_store(b, ARow{key.q2_lim}, rq, st, out + (size_t)e * key.n2w, key.n2w);
+  M.wide_mul_add_store(b, ARow{key.q2_lim}, rq, st, out ? out + (size_t)e * key.n2w : nullptr, key.n2w);
 }
 
 template <class MP2>
@@ -471,6 +583,47 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* 
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   if (e >= count) return;
   crt_enc_elem<MP2>(key, Np2, count, e, ws, out);
+}
+
+// k_crt_enc for one lane per residue with the ciphertext words written
+// through LDS: each lane packs 32 words of its element into the wave's tile
+// (row per lane, stride 33 words), then every store instruction writes two
+// whole 128-byte lines of consecutive ciphertexts (the lane-per-element form
+// scatters each store over 64 rows 512 bytes apart).
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_crt_enc_t(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
+                                                      uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
+  static_assert(MP2::TPI == 1, "one lane per residue");
+  constexpr int TS = 33;
+  __shared__ uint32_t tile_all[4][64 * TS];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t* tile = tile_all[(threadIdx.x >> 6) & 3];
+  const bool valid = e < count;
+  if (valid) crt_enc_elem<MP2>(key, Np2, count, e, ws, nullptr);
+  wave_sync_mem_();
+  const uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + e;  // this lane's 2S limbs, stride count
+  const int64_t e0 = e - lane;
+  const int nwords = key.n2w;
+  for (int c = 0; c < nwords; c += 32) {
+    if (valid) {
+      for (int j = 0; j < 32; ++j) {
+        const int bit = 32 * (c + j);
+        const int li = bit / MP2::W, sh = bit - li * MP2::W;
+        uint64_t v = 0;
+        if (li < 2 * MP2::S) v |= (uint64_t)rq[(size_t)li * count];
+        if (li + 1 < 2 * MP2::S) v |= (uint64_t)rq[(size_t)(li + 1) * count] << MP2::W;
+        if (li + 2 < 2 * MP2::S) v |= (uint64_t)rq[(size_t)(li + 2) * count] << (2 * MP2::W);
+        tile[lane * TS + j] = (uint32_t)(v >> sh);
+      }
+    }
+    wave_sync_mem_();
+    for (int r = 0; r < 32; ++r) {
+      const int el = 2 * r + (lane >> 5), wd = lane & 31;
+      if (e0 + el < count) out[(size_t)(e0 + el) * nwords + c + wd] = tile[el * TS + wd];
+    }
+    wave_sync_mem_();
+  }
 }
 
 // Raw encryption without obfuscation (paillier.py:283): c = 1 + n m  (m < n,
@@ -829,7 +982,7 @@ __global__ void __launch_bounds__(256, 2) k_powmod_n2(KeyDev key, const uint32_t
 
 // Public-key DJN encryption (paillier.py:210-212,283): (1 + n m) h^a mod n^2
 // with the fixed-base table of h mod n^2.
-template <class MN2>
+template <class MN2, int RW>
 __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* __restrict__ Nn2,
                                                     const uint32_t* __restrict__ m_words,
                                                     const uint32_t* __restrict__ a_words, int aw, int64_t count,
@@ -847,7 +1000,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* 
   for (int w = 0; w < key.nwin; ++w) {
     int bit = w * key.win;
     uint32_t d = digit_at(ae, aw, bit, key.win);
-    M.mul(b, ARow{key.tab_n2 + ((size_t)w * rows + d) * MN2::S4});
+    M.mul(b, ARowPacked<MN2::W, RW>{key.tab_n2 + ((size_t)w * rows + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -871,8 +1024,9 @@ XHE_DEV void nodjn_core(const M_& M, uint32_t (&b)[M_::L], const ModDev& md, con
   // r R, then r^e R
   M.load_words(b, rw, rwn);
   M.mul(b, ARow{md.R2});
-  const int nwin = (ebits + 3) / 4;
-  pow_window4(M, b, md.R1, nwin, [&](int w) { return nibble(ex, exw, w); }, tab, sq, st, sq_lds);
+  // the exponent (n or e_P) is the same for every lane: wave-uniform 5-bit
+  // sliding window (~ebits/6 table products instead of ebits/4)
+  pow_uniform_exp(M, b, ex, ebits, tab, sq, st, sq_lds);
   wave_sync_mem_();
   M.mul(b, AStrided{park, st});
   M.mul(b, AOne{});
@@ -1176,17 +1330,27 @@ __global__ void __launch_bounds__(256, 2) k_mexp_horner(KeyDev key, const uint32
 // ============================================================== tables
 // Fixed-base table for h (Montgomery form row `hM`, canonical):
 //   tab[w][d] = h^(d * 2^(win*w)) * R mod M, d in [0, 2^win)
-// k_tab_bases: one group walks the squaring chain, writing tab[w][1].
+// stored packed (RW words per row: K/32 mod p^2, K/16 mod n^2). Every row is a product of a "high"
+// and a "low" chain entry (d = hi * 2^half + lo): the chains are built first
+// in a limb-form scratch `chain` ([nwin][CH] rows of S4 limbs), then
+// k_tab_combine writes every packed row. Chain index of an entry: low d
+// (0 <= d <= 2^half) at d, high d (>= 1) at 2^half + d - 1 (high 1 = low 2^half).
+XHE_DEV int64_t chain_index(int64_t d, int sh, int half) { return sh == 0 ? d : ((int64_t)1 << half) + d - 1; }
+XHE_DEV int64_t chain_rows(int win) { return ((int64_t)1 << (win / 2)) + ((int64_t)1 << (win - win / 2)); }
+
+// k_tab_bases: one group walks the squaring chain, writing low entry 1 of
+// every window (h^(2^(win w)) R).
 template <class MP2>
-__global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* hM, int win, int nwin, uint32_t* tab, uint32_t* ws) {
+__global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* hM, int win, int nwin, uint32_t* chain,
+                                                     uint32_t* ws) {
   if (blockIdx.x != 0 || threadIdx.x >= MP2::TPI) return;
   MP2 M;
   M.init(md.N, md.n0inv);
   uint32_t b[MP2::L];
   M.load_row(b, hM);
-  const int rows = 1 << win;
+  const int64_t CH = chain_rows(win);
   for (int w = 0; w < nwin; ++w) {
-    M.store_row(b, tab + ((size_t)w * rows + 1) * MP2::S4);
+    M.store_row(b, chain + ((size_t)w * CH + 1) * MP2::S4);
     if (w + 1 == nwin) break;
     for (int s = 0; s < win; ++s) {
       M.store_row(b, ws);
@@ -1197,9 +1361,9 @@ __global__ void __launch_bounds__(64, 2) k_tab_bases(ModDev md, const uint32_t* 
   }
 }
 
-// tab[w][0] = R (the digit-0 row: Montgomery one), one group per window
+// low entry 0 = R (Montgomery one), one group per window
 template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_tab_one(ModDev md, int win, int nwin, uint32_t* __restrict__ tab) {
+__global__ void __launch_bounds__(256, 2) k_tab_one(ModDev md, int win, int nwin, uint32_t* __restrict__ chain) {
   const int w = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI);
   if (w >= nwin) return;
   MP2 M;
@@ -1207,31 +1371,39 @@ __global__ void __launch_bounds__(256, 2) k_tab_one(ModDev md, int win, int nwin
   uint32_t b[MP2::L];
   M.load_row(b, md.R1);
   M.reduce_once(b);
-  M.store_row(b, tab + ((size_t)w << win) * MP2::S4);
+  M.store_row(b, chain + (size_t)w * chain_rows(win) * MP2::S4);
 }
 
+// One doubling level of a chain (sh = 0: low, sh = half: high): entries
+// d in [per + 1, 2 per] as entry (d - per) * entry per, d < lim.
 template <class MP2>
 __global__ void __launch_bounds__(256, 2) k_tab_level(ModDev md, const uint32_t* __restrict__ Nm, int win, int nwin,
-                                                       int t, int sh, int lim, uint32_t* __restrict__ tab) {
+                                                       int t, int sh, int lim, uint32_t* __restrict__ chain) {
   const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   const int64_t per = (int64_t)1 << t;
   if (idx >= (int64_t)nwin * per) return;
   const int w = (int)(idx >> t);
   const int64_t d = per + 1 + (idx & (per - 1));
   if (d >= lim) return;
-  uint32_t* tw = tab + ((size_t)w << win) * MP2::S4;
+  const int half = win / 2;
+  uint32_t* cw = chain + (size_t)w * chain_rows(win) * MP2::S4;
   MP2 M;
   M.init(Nm, md.n0inv);
   uint32_t b[MP2::L];
-  M.load_row(b, tw + ((size_t)(d - per) << sh) * MP2::S4);
-  M.mul(b, ARow{tw + ((size_t)per << sh) * MP2::S4});
+  M.load_row(b, cw + (size_t)chain_index(d - per, sh, half) * MP2::S4);
+  M.mul(b, ARow{cw + (size_t)chain_index(per, sh, half) * MP2::S4});
   M.reduce_once(b);
-  M.store_row(b, tw + ((size_t)d << sh) * MP2::S4);
+  M.store_row(b, cw + (size_t)chain_index(d, sh, half) * MP2::S4);
 }
 
-template <class MP2>
+// Every packed row: a chain entry itself (lo == 0 or hi == 0) or the product
+// of its high and low entries. The packing goes through a per-group LDS row
+// (the group's limbs are spread over TPI lanes).
+template <class MP2, int RW>
 __global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, const uint32_t* __restrict__ Nm, int win,
-                                                         int nwin, uint32_t* __restrict__ tab) {
+                                                         int nwin, const uint32_t* __restrict__ chain,
+                                                         uint32_t* __restrict__ tab) {
+  __shared__ __attribute__((aligned(16))) uint32_t sc_all[(256 / MP2::TPI) * MP2::S4];
   const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   const int64_t rows = (int64_t)nwin << win;
   if (idx >= rows) return;
@@ -1239,15 +1411,23 @@ __global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, const uint32_
   const int w = (int)(idx >> win);
   const int d = (int)(idx & ((1 << win) - 1));
   const int lo = d & ((1 << half) - 1), hi = d >> half;
-  if (lo == 0 || hi == 0) return;  // chain entries
-  uint32_t* t = tab + ((size_t)w << win) * MP2::S4;
+  const uint32_t* cw = chain + (size_t)w * chain_rows(win) * MP2::S4;
   MP2 M;
   M.init(Nm, md.n0inv);
   uint32_t b[MP2::L];
-  M.load_row(b, t + ((size_t)hi << half) * MP2::S4);
-  M.mul(b, ARow{t + (size_t)lo * MP2::S4});
-  M.reduce_once(b);
-  M.store_row(b, t + (size_t)d * MP2::S4);
+  if (hi == 0) {
+    M.load_row(b, cw + (size_t)chain_index(lo, 0, half) * MP2::S4);
+  } else if (lo == 0) {
+    M.load_row(b, cw + (size_t)chain_index(hi, half, half) * MP2::S4);
+  } else {
+    M.load_row(b, cw + (size_t)chain_index(hi, half, half) * MP2::S4);
+    M.mul(b, ARow{cw + (size_t)chain_index(lo, 0, half) * MP2::S4});
+    M.reduce_once(b);
+  }
+  uint32_t* sc = sc_all + (size_t)((threadIdx.x % 256) / MP2::TPI) * MP2::S4;
+  M.store_row(b, sc);
+  wave_sync_mem_();
+  pack_words_<MP2::W, MP2::TPI>(sc, 1, MP2::S, tab + (size_t)idx * RW, RW);
 }
 
 // Montgomery product of two rows (host-side setup helper / unit tests):

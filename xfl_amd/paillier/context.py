@@ -1,3 +1,7 @@
+# Portions mirror the API of XFL (python/common/crypto/paillier), Copyright 2022
+# The XFL Authors, licensed under the Apache License, Version 2.0
+# (http://www.apache.org/licenses/LICENSE-2.0): the method names, arguments and
+# spec formulas of the drop-in interface follow that file.
 """PaillierContext — drop-in for python/common/crypto/paillier/context.py.
 
 Same constructor/init/generate/serialize surface and attribute names as the
