@@ -24,18 +24,22 @@ from tools.bench_configs import _encrypt_f64, _sync, _timed  # noqa: E402
 
 # elements per timed call: enough lanes to fill the chip in the batch shapes
 N_BY_BITS = {2048: 1_000_000, 3072: 500_000, 4096: 262_144, 8192: 65_536}
-WIN_BY_BITS = {2048: 22, 3072: 20, 4096: 18, 8192: 16}
+# --win 0: each size at the widest window whose packed tables leave 16 GiB of
+# HBM free (bench.pick_window), as bench.py --key-bits K picks it
 
 
-def run(bits, steps):
+def run(bits, steps, win):
     import torch
     from tests.conftest import hx, load_fixture
     from xfl_amd import _native as nat
     L = nat.lib()
     k = load_fixture(f"paillier_{bits}_djn.json")["key"]
     p, q, h = hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
+    if not win:
+        from bench import pick_window
+        win = pick_window(bits, torch.cuda.mem_get_info(0)[0])
     t0 = time.time()
-    dk = nat.DeviceKey(bits, p * q, p, q, h, device=0, win_bits=WIN_BY_BITS[bits])
+    dk = nat.DeviceKey(bits, p * q, p, q, h, device=0, win_bits=win)
     _sync()
     tk = time.time() - t0
     N = N_BY_BITS[bits]
@@ -53,8 +57,8 @@ def run(bits, steps):
     # SURVEY 8(d) model: 2 nwin table products of s = K/32 limbs at 2s^2+s
     # MACs (bench.py's roofline.achieved), over the measured v_mad peak
     s_ = bits // 32
-    macs = 2 * (-(-dk.rand_bits // WIN_BY_BITS[bits])) * (2 * s_ * s_ + s_)
-    out = {"key_bits": bits, "elements": N, "fixed_base_window_bits": WIN_BY_BITS[bits],
+    macs = 2 * (-(-dk.rand_bits // win)) * (2 * s_ * s_ + s_)
+    out = {"key_bits": bits, "elements": N, "fixed_base_window_bits": win,
            "encrypts_per_s": N / te, "decrypts_per_s": N / td,
            "alg_macs_per_encrypt": macs, "encrypt_tmac_per_s": N / te * macs / 1e12,
            "encrypt_roofline_frac": N / te * macs / 39.3216e12,
@@ -68,9 +72,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bits", default="2048,3072,4096,8192")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--win", type=int, default=0, help="window bits for every size; 0 = widest that fits")
     a = ap.parse_args()
     for b in [int(v) for v in a.bits.split(",")]:
-        print(json.dumps(run(b, a.steps)), flush=True)
+        print(json.dumps(run(b, a.steps, a.win)), flush=True)
 
 
 if __name__ == "__main__":
