@@ -89,8 +89,11 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
     priv = key if key is not None else Paillier.context(2048, djn_on=True)
     pub_bytes = priv.to_public().serialize()
     pub = Paillier.context_from(pub_bytes)
+    t_gen = time.time() - t0
+    t1 = time.time()
     priv.device_key()  # device constants + fixed-base tables, once per key (fit)
     pub.device_key()
+    t_dev = time.time() - t1
     t_key = time.time() - t0
     okey = None
     if check:
@@ -147,7 +150,8 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
             bias -= lr * -np.mean(resid)
             batches += 1
         epoch_tm.append(({k: tm[k] - before[k] for k in tm}, batches - nb0))
-    rec = {"batches": batches, "checked_bit_exact": checked, "key_s": t_key,
+    rec = {"batches": batches, "checked_bit_exact": checked, "key_s": t_key, "keygen_s": t_gen,
+           "device_key_s": t_dev, "device_window_bits": priv.device_key().win_bits,
            "phase_s": tm, "he_total_s": sum(tm.values()),
            "per_batch_ms": {k: 1e3 * v / max(batches, 1) for k, v in tm.items()}}
     if len(epoch_tm) > 1:
