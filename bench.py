@@ -44,13 +44,15 @@ def make_key(bits, seed):
     return p, q, n, h_pow_n
 
 
-def algorithmic_macs_per_element(bits, win, rand_bits):
+def algorithmic_macs_per_element(bits, win_bits, rand_bits):
     """32-bit-limb MACs of the fixed-base DJN-CRT encryption (SURVEY 8(d) model):
     per prime 1 (n m R) + nwin table products + 1 (from Montgomery) CIOS
     products of s = bits/32 limbs at 2s^2+s MACs each; plus the CRT product and
-    the q^2 * h wide multiply (s^2)."""
+    the q^2 * h wide multiply (s^2). Second value: the table products alone
+    (the dominant kernel's model work)."""
+    from xfl_amd._native import win_layout
     s = bits // 32
-    nwin = -(-rand_bits // win)
+    nwin, _ = win_layout(rand_bits, win_bits)
     prod = 2 * s * s + s
     return 2 * (nwin + 2) * prod + prod + s * s, 2 * nwin * prod
 
@@ -85,33 +87,45 @@ def cpu_baseline(bits, seconds, cores):
 TABLE_ROW_BYTES = {2048: 256, 3072: 384, 4096: 512, 8192: 1024}  # packed rows: K/32 words x 4 (xhe.hip Shape<K>::RW)
 
 
-def table_bytes(bits, win):
-    """Device bytes of the two fixed-base tables (xhe_key_create, include/xhe.h):
-    ceil(rand_bits/win) windows x 2^win packed rows of K/32 words per prime."""
-    rand_bits = bits // 2
-    return 2 * -(-rand_bits // win) * (1 << win) * TABLE_ROW_BYTES[bits]
+def table_bytes(bits, win_bits):
+    """Device bytes of the two fixed-base tables (xhe_key_create, include/xhe.h)."""
+    from xfl_amd._native import table_bytes as tb
+    return tb(bits, win_bits)
 
 
-def pick_window(bits, free_bytes, margin=16 << 30):
-    """Widest window (<= 23) whose tables leave `margin` of HBM free."""
-    for w in range(23, 11, -1):
-        if table_bytes(bits, w) + margin <= free_bytes:
-            return w
-    return 12
+def pick_window(bits, free_bytes, margin=16 << 30, split=False):
+    """The window layout with the fewest table products per element whose
+    tables leave `margin` of HBM free (ties: fewer bytes): uniform w <= 24,
+    and with split=True also split w <= 23 (include/xhe.h XHE_WIN_SPLIT).
+    Split layouts are not the default: at 2048 bits 23s (44 products, 240 GB)
+    measured only 1.0 % faster than 23 (45, 193 GB) - its 2^24-row windows
+    cost more per random row - for 25 % more table memory and build time."""
+    from xfl_amd._native import XHE_WIN_SPLIT, win_layout
+    best = None
+    for w in range(12, 25):
+        for wb in (w, w | XHE_WIN_SPLIT) if split and w <= 23 else (w,):
+            nb = table_bytes(bits, wb)
+            if nb + margin > free_bytes:
+                continue
+            key = (win_layout(bits // 2, wb)[0], nb)
+            if best is None or key < best[0]:
+                best = (key, wb)
+    return best[1] if best else 12
 
 
-def pmc_traffic(win, n):
+def pmc_traffic(win_bits, n):
     """HBM bytes per k_djn_pow launch from the committed rocprofv3 PMC passes
     (tools/profile_box.sh -> tools/pmc_traffic.py), when they were taken on
     this configuration; else None. Counters cannot be read inside this run
     (rocprofv3 --pmc is its own pass)."""
+    from xfl_amd._native import win_spec
     path = os.path.join(ROOT, "profiles", "r2", "k_djn_pow_pmc.json")
     try:
         with open(path) as f:
             rec = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if rec.get("win") != win or rec.get("n") != n or "traffic_bytes" not in rec:
+    if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
         return None, None
     return rec["traffic_bytes"], os.path.relpath(path, ROOT)
 
@@ -292,9 +306,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="elements per GPU")
     ap.add_argument("--key-bits", type=int, default=2048)
-    ap.add_argument("--win", type=int, default=0,
-                    help="fixed-base window bits; 0 = the widest of 23 (2 x 114.8 GB tables, 45 products per prime) "
-                         "and 22 (2 x 59.9 GB, 47) whose tables leave 16 GiB of the GPU free")
+    ap.add_argument("--win", default="0",
+                    help="fixed-base window: w or ws (split, XHE_WIN_SPLIT); 0 = the uniform window with the fewest "
+                         "table products whose tables leave 16 GiB of the GPU free (2048 bits: 23, 2 x 96.6 GB, 45 "
+                         "products per prime)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
@@ -322,6 +337,7 @@ def main():
 
     bits = args.key_bits
     p, q, n, h = make_key(bits, seed=2024)
+    args.win = nat.parse_win(args.win)
     if args.win == 0:
         args.win = pick_window(bits, torch.cuda.mem_get_info(local)[0])
     t_key = time.time()
@@ -409,13 +425,14 @@ def main():
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"DJN private-key (CRT) encrypt, obfuscated, precision 7, {N} float64 "
                                    f"plaintexts/GPU resident in HBM" + (", + RCCL all-gather" if world > 1 else ""),
-                       "key_bits": bits, "elements_per_gpu": N, "fixed_base_window_bits": args.win,
+                       "key_bits": bits, "elements_per_gpu": N, "fixed_base_window_bits": args.win & 0xFF,
+                       "fixed_base_window_split": bool(args.win & nat.XHE_WIN_SPLIT),
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "valu-int", "achieved": achieved, "peak": PEAK_MAC_PER_S / 1e12,
                          "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": kname, "kernel_avg_ms": pow_avg_s * 1e3,
                          "alg_macs_per_element": w_pow,
-                         "alg_table_bytes_per_launch": N * 2 * -(-dk.rand_bits // args.win) * TABLE_ROW_BYTES[bits]},
+                         "alg_table_bytes_per_launch": N * 2 * nat.win_layout(dk.rand_bits, args.win)[0] * TABLE_ROW_BYTES[bits]},
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,
         }

@@ -30,14 +30,17 @@ typedef struct xhe_key xhe_key;
 
 /* Key material -> device key handle with all per-key precomputes
  * (PaillierContext.init, context.py:28-71) and, for a DJN private key, the
- * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win_bits rows per window).
+ * fixed-base tables of h_pow_n mod p^2 / q^2 (2^win rows per window).
  * p_words/q_words NULL => public key (n only). h_pow_n_words NULL => DJN off.
- * p, q: nw/2 words each; h_pow_n: n2w words. win_bits in [2, 24];
- * 0 = default (16, or $XHE_WIN_BITS). Tables take ceil(rand_bits/win) x
- * 2^win rows of S4 words per prime: 2048-bit key, win 16: 2 x 1.28 GB;
- * win 20: 2 x 16.6 GB (52 instead of 64 products per prime); win 22:
- * 2 x 59.9 GB (47); win 23: 2 x 114.8 GB (45); 4096-bit key, win 16:
- * 2 x 5.1 GB. key_bits: 2048, 3072, 4096 or 8192 (else XHE_ENOTSUP). */
+ * p, q: nw/2 words each; h_pow_n: n2w words. win_bits: the window w in
+ * [2, 24], 0 = default (16, or $XHE_WIN_BITS); tables take ceil(rand_bits/w)
+ * windows of 2^w packed rows (K/32 words) per prime. With XHE_WIN_SPLIT or'ed
+ * in (w <= 23): floor(rand_bits/w) windows, the first rand_bits mod w of them
+ * w+1 bits wide (one table product fewer for ~1.25x the rows). 2048-bit key
+ * (rand_bits 1024), per prime: w 16: 1.07 GB, 64 products; 20: 14 GB, 52;
+ * 22: 50.5 GB, 47; 23: 96.6 GB, 45; 23 split: 120.3 GB, 44.
+ * key_bits: 2048, 3072, 4096 or 8192 (else XHE_ENOTSUP). */
+#define XHE_WIN_SPLIT 0x100
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out);
 void xhe_key_destroy(xhe_key* key);

@@ -127,3 +127,27 @@ def test_table_window_policy(monkeypatch):
     assert pub.device_key().win_bits == 0
     nodjn, _ = C.ctxs(load_fixture("paillier_2048_nodjn.json"))
     assert nodjn.device_key().win_bits == 0
+
+
+def test_window_layouts():
+    """Split table layouts (include/xhe.h XHE_WIN_SPLIT): floor(rand_bits/w)
+    windows, the first rand_bits mod w of them w+1 bits wide; the bench picks
+    the uniform layout with the fewest table products that fits (split ones
+    on request)."""
+    import bench
+    from xfl_amd._native import XHE_WIN_SPLIT as S
+    from xfl_amd._native import parse_win, table_bytes, win_layout, win_spec
+    assert win_layout(1024, 23) == (45, 0) and win_layout(1024, 23 | S) == (44, 12)
+    assert win_layout(1024, 16 | S) == (64, 0)  # divides evenly: uniform
+    for rb, wb in ((1024, 23 | S), (1536, 22), (2048, 21 | S), (1024, 7 | S)):
+        nwin, nhi = win_layout(rb, wb)
+        w = wb & 0xFF
+        assert nhi * (w + 1) + (nwin - nhi) * w == rb or (nhi == 0 and nwin * w >= rb)
+    assert table_bytes(2048, 23) == 2 * 45 * (1 << 23) * 256
+    assert table_bytes(2048, 23 | S) == 2 * 56 * (1 << 23) * 256
+    assert parse_win("23s") == 23 | S and parse_win("22") == 22 and win_spec(23 | S) == "23s"
+    assert bench.pick_window(2048, 287 * 10**9) == 23
+    assert bench.pick_window(2048, 287 * 10**9, split=True) == 23 | S
+    assert bench.pick_window(2048, 230 * 10**9, split=True) == 23  # 240.5 GB + 16 GiB does not fit
+    assert bench.pick_window(3072, 287 * 10**9, split=True) == 22
+    assert bench.pick_window(4096, 287 * 10**9) == 21

@@ -97,16 +97,20 @@ def test_multiexp_both_shapes(ctx, nbases, ncols):
 def test_djn_encrypt_both_shapes():
     """DJN private encryption: the 16-lane small-batch kernel (k_djn_pow_x, on
     the one-lane tables with the (R'/R)^nwin start factor) and the one-lane
-    kernel give identical ciphertexts, equal to the closed form."""
+    kernel give identical ciphertexts, equal to the closed form - with uniform
+    windows and with split layouts (XHE_WIN_SPLIT: the first rand_bits mod w
+    windows w+1 bits wide, their tables built as a second segment)."""
     from oracle import paillier_oracle as O
-    from xfl_amd._native import DeviceKey, ints_to_words, words_to_ints
+    from xfl_amd._native import XHE_WIN_SPLIT, DeviceKey, ints_to_words, win_layout, words_to_ints
     for fx in FIXTURES:
         g = load_fixture(fx)
         k = g["key"]
         if not k["djn_on"]:
             continue
         n, p, q, h = hx(k["n"]), hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
-        for win in (16, 7):
+        for win in (16, 7, 7 | XHE_WIN_SPLIT, 10 | XHE_WIN_SPLIT):
+            if win & XHE_WIN_SPLIT:
+                assert win_layout(g["key_bits"] // 2, win)[1] > 0  # really split
             dk = DeviceKey(g["key_bits"], n, p, q, h, win_bits=win)
             rng = random.Random(win)
             nbig = 24000  # above the 16-lane encryption limit (20,480)

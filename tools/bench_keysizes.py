@@ -57,8 +57,8 @@ def run(bits, steps, win):
     # SURVEY 8(d) model: 2 nwin table products of s = K/32 limbs at 2s^2+s
     # MACs (bench.py's roofline.achieved), over the measured v_mad peak
     s_ = bits // 32
-    macs = 2 * (-(-dk.rand_bits // win)) * (2 * s_ * s_ + s_)
-    out = {"key_bits": bits, "elements": N, "fixed_base_window_bits": win,
+    macs = 2 * nat.win_layout(dk.rand_bits, win)[0] * (2 * s_ * s_ + s_)
+    out = {"key_bits": bits, "elements": N, "fixed_base_window": nat.win_spec(win),
            "encrypts_per_s": N / te, "decrypts_per_s": N / td,
            "alg_macs_per_encrypt": macs, "encrypt_tmac_per_s": N / te * macs / 1e12,
            "encrypt_roofline_frac": N / te * macs / 39.3216e12,
@@ -72,10 +72,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bits", default="2048,3072,4096,8192")
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--win", type=int, default=0, help="window bits for every size; 0 = widest that fits")
+    ap.add_argument("--win", default="0", help="window for every size (w or ws = split); 0 = fewest products that fit")
     a = ap.parse_args()
     for b in [int(v) for v in a.bits.split(",")]:
-        print(json.dumps(run(b, a.steps, a.win)), flush=True)
+        from xfl_amd._native import parse_win
+        print(json.dumps(run(b, a.steps, parse_win(a.win))), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 PMC passes of bench.py (tools/profile_box.sh output) for
 one kernel into the per-launch JSON that bench.py reports as roofline.traffic.
 
-    python tools/pmc_traffic.py gpurun_out/<tag> profiles/r1/k_djn_pow_pmc.json [--kernel k_djn_pow]
+    python tools/pmc_traffic.py gpurun_out/<tag> profiles/r2/k_djn_pow_pmc.json --win 23 --n 1000000 [--kernel k_djn_pow]
 
 Units and corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE
 and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-B
@@ -47,9 +47,10 @@ def main():
                     vals[c].append(v)
     avg = {c: sum(v) / len(v) for c, v in vals.items()}
     rec = {"kernel": kernel, "grid_size": grid_max, "counters_per_launch": avg}
-    for opt in ("--win", "--n"):
-        if opt in sys.argv:
-            rec[opt[2:]] = int(sys.argv[sys.argv.index(opt) + 1])
+    if "--win" in sys.argv:  # window spec as bench.py --win takes it: "23" or "23s" (split)
+        rec["win"] = sys.argv[sys.argv.index("--win") + 1]
+    if "--n" in sys.argv:
+        rec["n"] = int(sys.argv[sys.argv.index("--n") + 1])
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         fetch = 2 * avg["FETCH_SIZE"] * 1024
         write = avg["WRITE_SIZE"] * 1024

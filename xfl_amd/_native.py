@@ -190,12 +190,37 @@ def ptr(a):
 TABLE_ROW_WORDS = {2048: 64, 3072: 96, 4096: 128, 8192: 256}  # packed rows: xhe.hip Shape<K>::RW = K/32
 
 
+XHE_WIN_SPLIT = 0x100  # include/xhe.h: floor(rand_bits/w) windows, the first rand_bits mod w of them w+1 bits
+
+
+def win_layout(rand_bits, win_bits):
+    """(windows, wide windows) of a fixed-base table (xhe.hip win_layout):
+    ceil(rand_bits/w) windows of w bits, or with XHE_WIN_SPLIT floor(rand_bits/w)
+    windows of which the first rand_bits mod w are w+1 bits wide."""
+    w = win_bits & 0xFF
+    if win_bits & XHE_WIN_SPLIT and rand_bits % w and rand_bits % w <= rand_bits // w:
+        return rand_bits // w, rand_bits % w
+    return -(-rand_bits // w), 0
+
+
+def win_spec(win_bits):
+    """'23' / '23s' (split) - the text form of a window choice."""
+    return f"{win_bits & 0xFF}{'s' if win_bits & XHE_WIN_SPLIT else ''}"
+
+
+def parse_win(spec):
+    """Inverse of win_spec; also accepts plain ints."""
+    spec = str(spec).strip()
+    return int(spec[:-1]) | XHE_WIN_SPLIT if spec.endswith("s") else int(spec)
+
+
 def table_bytes(key_bits, win_bits):
-    """Device bytes of a DJN private key's two fixed-base tables: ceil(rand_bits
-    / win) windows x 2^win packed rows of K/32 words per prime (rand_bits = K/2)."""
+    """Device bytes of a DJN private key's two fixed-base tables: per prime
+    (windows + wide windows) x 2^w packed rows of K/32 words (rand_bits = K/2)."""
     if not win_bits:
         return 0
-    return 2 * -(-(key_bits // 2) // win_bits) * (1 << win_bits) * TABLE_ROW_WORDS[key_bits] * 4
+    nwin, nhi = win_layout(key_bits // 2, win_bits)
+    return 2 * (nwin + nhi) * (1 << (win_bits & 0xFF)) * TABLE_ROW_WORDS[key_bits] * 4
 
 
 def device_free_bytes(device=0):
@@ -231,7 +256,9 @@ class DeviceKey:
         self.private = bool(flags & 1)
         self.djn = bool(flags & 2)
         self.device = device
-        self.win_bits = (win_bits or int(os.environ.get("XHE_WIN_BITS", "0") or 16)) if self.private and self.djn else 0
+        wb = (win_bits or int(os.environ.get("XHE_WIN_BITS", "0") or 16)) if self.private and self.djn else 0
+        self.win_bits = wb & 0xFF  # the window w
+        self.win_split = bool(wb & XHE_WIN_SPLIT)
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -179,15 +179,30 @@ template <class MP2, int RW>
 void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
                     uint32_t* d_ws, hipStream_t s);
 
+// Window layout of a fixed-base table over rand_bits exponent bits: uniform
+// ceil(rand_bits/win) windows, or (split) floor(rand_bits/win) windows of
+// which the first rand_bits mod win are win+1 bits wide (KeyDev::nhi).
+void win_layout(int rand_bits, int win, bool split, int* nwin, int* nhi) {
+  *nwin = (rand_bits + win - 1) / win;
+  *nhi = 0;
+  if (split && rand_bits % win != 0 && rand_bits % win <= rand_bits / win) {
+    *nwin = rand_bits / win;
+    *nhi = rand_bits % win;
+  }
+}
+
+int64_t chain_rows_h(int win) { return ((int64_t)1 << (win / 2)) + ((int64_t)1 << (win - win / 2)); }
+
 // Tables of one modulus, or of p^2 and q^2 concurrently on two streams.
 template <class MP2, int RW>
 void build_tables_sync(xhe_key* k, const ModDev* md, const uint32_t* const* d_hM, uint32_t* const* d_tab, int count) {
   hipStream_t st[2] = {nullptr, nullptr};
   uint32_t* ws[2] = {nullptr, nullptr};
   uint32_t* chain[2] = {nullptr, nullptr};
-  const int win = k->kd.win;
+  const int win = k->kd.win, nwin = k->kd.nwin, nhi = k->kd.nhi;
   const size_t chain_words =
-      (size_t)k->kd.nwin * (((size_t)1 << (win / 2)) + ((size_t)1 << (win - win / 2))) * MP2::S4;
+      (size_t)std::max<int64_t>(nhi ? (nhi + 1) * chain_rows_h(win + 1) : 0, (nwin - nhi) * chain_rows_h(win)) *
+      MP2::S4;
   for (int i = 0; i < count; ++i) {
     HIPCHK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
     HIPCHK(hipMalloc(&ws[i], MP2::S4 * sizeof(uint32_t) * 4));
@@ -202,16 +217,18 @@ void build_tables_sync(xhe_key* k, const ModDev* md, const uint32_t* const* d_hM
   }
 }
 
-// Fixed-base table build, enqueued on `s` (no synchronisation; d_ws and
-// d_chain must stay alive until s has drained): bases (low entry 1 of every
-// window) = h^(2^(win w)) by one squaring chain, every window's low and high
-// chains by doubling levels (k_tab_level: log2 depth instead of 2^(win/2)),
-// then every packed row as one product of a high and a low entry.
+// One uniform table segment (nwin windows of win bits starting at base
+// d_base), enqueued on `s` (no synchronisation; d_ws and d_chain must stay
+// alive until s has drained): window bases (low entry 1 of every window) =
+// base^(2^(win w)) by one squaring chain over nbases >= nwin windows, every
+// window's low and high chains by doubling levels (k_tab_level: log2 depth
+// instead of 2^(win/2)), then every packed row as one product of a high and a
+// low entry.
 template <class MP2, int RW>
-void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
-                    uint32_t* d_ws, hipStream_t s) {
-  const int win = k->kd.win, nwin = k->kd.nwin, half = win / 2;
-  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_hM, win, nwin, d_chain, d_ws);
+void build_tables_seg(const ModDev& md, const uint32_t* d_base, int win, int nwin, int nbases, uint32_t* d_tab,
+                      uint32_t* d_chain, uint32_t* d_ws, hipStream_t s) {
+  const int half = win / 2;
+  hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_base, win, nbases, d_chain, d_ws);
   HIPCHK(hipGetLastError());
   auto blocks = [&](int64_t groups) { return dim3((unsigned)std::max<int64_t>(1, (groups * MP2::TPI + 255) / 256)); };
   hipLaunchKernelGGL(k_tab_one<MP2>, blocks(nwin), dim3(256), 0, s, md, win, nwin, d_chain);
@@ -230,6 +247,25 @@ void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t
   int64_t rows = (int64_t)nwin << win;
   hipLaunchKernelGGL((k_tab_combine<MP2, RW>), blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_chain, d_tab);
   HIPCHK(hipGetLastError());
+}
+
+// A key's tables (layout win_layout / win_digit): uniform, or the nhi wide
+// windows first, whose base chain runs one window further to
+// h^(2^(nhi (win+1))), the base of the narrow windows that follow.
+template <class MP2, int RW>
+void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
+                    uint32_t* d_ws, hipStream_t s) {
+  const int win = k->kd.win, nwin = k->kd.nwin, nhi = k->kd.nhi;
+  if (nhi == 0) {
+    build_tables_seg<MP2, RW>(md, d_hM, win, nwin, nwin, d_tab, d_chain, d_ws, s);
+    return;
+  }
+  uint32_t* base2 = d_ws + 2 * MP2::S4;  // d_ws rows: 0 = squaring scratch, 2 = the narrow windows' base
+  build_tables_seg<MP2, RW>(md, d_hM, win + 1, nhi, nhi + 1, d_tab, d_chain, d_ws, s);
+  HIPCHK(hipMemcpyAsync(base2, d_chain + ((size_t)nhi * chain_rows_h(win + 1) + 1) * MP2::S4,
+                        MP2::S4 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  build_tables_seg<MP2, RW>(md, base2, win, nwin - nhi, nwin - nhi, d_tab + ((size_t)nhi << (win + 1)) * RW, d_chain,
+                            d_ws, s);
 }
 
 ModDev moddev(uint32_t* base, const ModOff& o) {
@@ -304,7 +340,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       o.hM_p2 = bl.put_limbs(mulmod(mod(*h, p2), Rp2, p2), s2);  // h_pow_n mod p^2 (context.py:63)
       o.hM_q2 = bl.put_limbs(mulmod(mod(*h, q2), Rq2, q2), s2);
       // 16-lane small-batch shape on the same tables (k_djn_pow_x)
-      const int nwin = (k->rand_bits + win - 1) / win;
+      int nwin, nhi;
+      win_layout(k->rand_bits, win & 0xff, (win & XHE_WIN_SPLIT) != 0, &nwin, &nhi);
       const ModSpec& sx = k->mp2X;
       BigU Rx = pow2((size_t)sx.W * sx.S);
       BigU Cexp = pow2((size_t)(sx.S - s2.S) * s2.W * nwin);  // (R'/R)^nwin
@@ -409,9 +446,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.ep_bits = ep_bits;
     kd.eq_bits = eq_bits;
     if (k->djn) {
-      kd.win = win;
-      kd.nwin = (k->rand_bits + win - 1) / win;
-      size_t rows = (size_t)kd.nwin << win;
+      kd.win = win & 0xff;
+      win_layout(k->rand_bits, kd.win, (win & XHE_WIN_SPLIT) != 0, &kd.nwin, &kd.nhi);
+      size_t rows = (size_t)(kd.nwin + kd.nhi) << kd.win;
       size_t tab_words = rows * (size_t)(K / 32);  // packed rows: Shape::RW = K/32 words (p^2 < 2^K)
       HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
       kd.tab_p2 = k->d_tab;
@@ -426,9 +463,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     }
   }
   if (!k->priv && k->djn) {
-    kd.win = win;
-    kd.nwin = (k->rand_bits + win - 1) / win;
-    size_t rows = (size_t)kd.nwin << win;
+    kd.win = win & 0xff;
+    win_layout(k->rand_bits, kd.win, false, &kd.nwin, &kd.nhi);  // public tables stay uniform
+    size_t rows = (size_t)kd.nwin << kd.win;
     size_t tab_words = rows * (size_t)(K / 16);  // packed rows: Shape::RW2 = n2w words
     HIPCHK(hipMalloc(&k->d_tab, tab_words * sizeof(uint32_t)));
     kd.tab_n2 = k->d_tab;
@@ -498,11 +535,12 @@ bool enc_row(int64_t count) {
 
 // CRT of the two prime rows in ws into ciphertext words (k_crt_enc; the
 // one-lane shape writes through LDS so its stores are whole lines)
-template <class MP2>
+template <class Sh, class MP2 = typename Sh::MP2>
 void crt_enc_launch(const xhe_key* k, int64_t n, uint32_t* ws, uint32_t* ct, hipStream_t s) {
   const int blocks = (int)((n * MP2::TPI + 255) / 256);
   if constexpr (MP2::TPI == 1)
-    hipLaunchKernelGGL(k_crt_enc_t<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws, ct);
+    hipLaunchKernelGGL((k_crt_enc_w<MP2, 2 * Sh::K / 32>), dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws,
+                       ct);
   else
     hipLaunchKernelGGL(k_crt_enc<MP2>, dim3(blocks), dim3(256), 0, s, k->kd, k->kd.p2.N, n, ws, ct);
   HIPCHK(hipGetLastError());
@@ -537,7 +575,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
                          r + (size_t)off * k->rand_words, k->rand_words, n, ws);
       HIPCHK(hipGetLastError());
     }
-    crt_enc_launch<MP2>(k, n, ws, ct + (size_t)off * k->n2w, s);
+    crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
   }
   HIPCHK(hipFreeAsync(ws, s));
 }
@@ -591,7 +629,7 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
                            m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, rows, ws);
         HIPCHK(hipGetLastError());
       }
-      crt_enc_launch<MP2>(k, n, rows, ct + (size_t)off * k->n2w, s);
+      crt_enc_launch<Sh>(k, n, rows, ct + (size_t)off * k->n2w, s);
     }
     HIPCHK(hipFreeAsync(ws, s));
     HIPCHK(hipFreeAsync(rows, s));
@@ -1031,8 +1069,9 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
       const char* ev = getenv("XHE_WIN_BITS");
       win_bits = ev ? atoi(ev) : 16;
     }
-    if (win_bits < 2 || win_bits > 24)
-      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be in [2, 24]");
+    const int wbase = win_bits & ~XHE_WIN_SPLIT;
+    if (wbase < 2 || wbase > ((win_bits & XHE_WIN_SPLIT) ? 23 : 24))
+      return fail(XHE_EINVAL, "xhe_key_create: win_bits must be in [2, 24] (split: [2, 23])");
     std::unique_ptr<xhe_key> k(new xhe_key());
     k->device = device;
     k->K = key_bits;

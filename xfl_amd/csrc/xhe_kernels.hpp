@@ -54,9 +54,9 @@ struct KeyDev {
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
   const uint32_t* q2_lim;     // q^2 (MP2 limbs)
   const uint32_t* p2x4_lim;   // 4 p^2 (MP2 limbs)
-  const uint32_t* tab_p2;     // [nwin][2^win][S4] h^(d*2^(win*w)) * R mod p^2
+  const uint32_t* tab_p2;     // h^(d*2^bit(w)) * R mod p^2, packed rows, windows as win_loc()
   const uint32_t* tab_q2;
-  int win, nwin;
+  int win, nwin, nhi;         // nhi: the first nhi windows are win+1 bits wide (0: uniform)
   // ---- mod p / q (shape MP), decrypt
   ModDev p, q;
   const uint32_t* pm1_words;  // p - 1 (nw/2 words)
@@ -356,6 +356,15 @@ XHE_DEV uint32_t digit_at(const uint32_t* w, int nwords, int bit, int win) {
   return (uint32_t)(v >> sh) & ((1u << win) - 1u);
 }
 
+// Window w of a key's fixed-base tables: the first key.nhi windows are win+1
+// bits wide (2^(win+1) rows each), the rest win bits; returns the window's
+// digit of the exponent and sets row0 to its first table row. Wave-uniform.
+XHE_DEV uint32_t win_digit(const KeyDev& key, const uint32_t* a, int aw, int w, int64_t& row0) {
+  const int wide = w < key.nhi ? w : key.nhi;
+  row0 = (int64_t)(w + wide) << key.win;
+  return digit_at(a, aw, w * key.win + wide, key.win + (w < key.nhi ? 1 : 0));
+}
+
 // ---------------------------------------------------------------------------
 // Encryption, DJN private key (CRT over p^2, q^2)   (paillier.py:193-209, 283)
 //   c_P = (1 + n m) * h_P^a mod P^2        k_djn_pow, grid.y = prime (0: p, 1: q)
@@ -382,11 +391,10 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   M.mul(b, ARow{prime ? key.nR2_q2 : key.nR2_p2});  // n m R mod P^2
   M.add_row(b, md.R1);                              // (1 + n m) R
   const uint32_t* ae = a_words + (size_t)e * aw;
-  const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
-    int bit = w * key.win;
-    uint32_t d = digit_at(ae, aw, bit, key.win);
-    M.mul(b, ARowPacked<MP2::W, RW>{tab + ((size_t)w * rows + d) * RW});
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    M.mul(b, ARowPacked<MP2::W, RW>{tab + (size_t)(row0 + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -452,10 +460,10 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow_x(KeyDev key, const uint32_t
   M.mul(b, ARow{prime ? key.nR2C_q2X : key.nR2C_p2X});  // n m C R'
   M.add_row(b, prime ? key.R1C_q2X : key.R1C_p2X);     // (1 + n m) C R'
   const uint32_t* ae = a_words + (size_t)e * aw;
-  const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
-    uint32_t d = digit_at(ae, aw, w * key.win, key.win);
-    M.mul(b, ARowPacked<MX::W, RW>{tab + ((size_t)w * rows + d) * RW});
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    M.mul(b, ARowPacked<MX::W, RW>{tab + (size_t)(row0 + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -493,10 +501,10 @@ XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, c
   M.init(Np, md.n0inv);
   uint32_t b[MP2::L];
   const uint32_t* ae = a_words + (size_t)e * aw;
-  const int rows = 1 << key.win;
   auto stage = [&](int w) {
-    const uint32_t d = digit_at(ae, aw, w * key.win, key.win);
-    const uint32_t* row = tab + ((size_t)w * rows + d) * RW;
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    const uint32_t* row = tab + (size_t)(row0 + d) * RW;
 #pragma unroll
     for (int k = 0; k < RW / 4; ++k)
       __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
@@ -585,45 +593,83 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc(KeyDev key, const uint32_t* 
   crt_enc_elem<MP2>(key, Np2, count, e, ws, out);
 }
 
-// k_crt_enc for one lane per residue with the ciphertext words written
-// through LDS: each lane packs 32 words of its element into the wave's tile
-// (row per lane, stride 33 words), then every store instruction writes two
-// whole 128-byte lines of consecutive ciphertexts (the lane-per-element form
-// scatters each store over 64 rows 512 bytes apart).
-template <class MP2>
-__global__ void __launch_bounds__(256, 2) k_crt_enc_t(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
-                                                      uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
+// k_crt_enc for one lane per residue, the wide product c_q + q^2 t streamed
+// straight into ciphertext words: every limb of the low half is final as
+// soon as its row of the operand scan retires, the high half after one
+// normalisation, so the limbs are packed into 32-bit words in registers and
+// the words go to a per-wave LDS ring (64 words per lane, stride 65); every
+// 32 words the ring is stored as whole 128-byte lines of consecutive
+// ciphertexts (two per store instruction). Nothing goes back through the
+// global workspace (the strided form writes the 2S limbs to ws and reads
+// them back to pack them). The word bookkeeping (bits pending, words out) is
+// wave-uniform, so its branches are scalar.
+template <class MP2, int NW2>
+__global__ void __launch_bounds__(256, 2) k_crt_enc_w(KeyDev key, const uint32_t* __restrict__ Np2, int64_t count,
+                                                      const uint32_t* __restrict__ ws, uint32_t* __restrict__ out) {
   static_assert(MP2::TPI == 1, "one lane per residue");
-  constexpr int TS = 33;
-  __shared__ uint32_t tile_all[4][64 * TS];
+  constexpr int S = MP2::S, W = MP2::W, RS = 65;
+  static_assert(NW2 % 32 == 0 && 2 * S * W >= 32 * NW2, "ciphertext words");
+  __shared__ uint32_t ring_all[4][64 * RS];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = (int)(threadIdx.x & 63);
-  uint32_t* tile = tile_all[(threadIdx.x >> 6) & 3];
-  const bool valid = e < count;
-  if (valid) crt_enc_elem<MP2>(key, Np2, count, e, ws, nullptr);
-  wave_sync_mem_();
-  const uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + e;  // this lane's 2S limbs, stride count
+  uint32_t* ring = ring_all[(threadIdx.x >> 6) & 3];
   const int64_t e0 = e - lane;
-  const int nwords = key.n2w;
-  for (int c = 0; c < nwords; c += 32) {
-    if (valid) {
-      for (int j = 0; j < 32; ++j) {
-        const int bit = 32 * (c + j);
-        const int li = bit / MP2::W, sh = bit - li * MP2::W;
-        uint64_t v = 0;
-        if (li < 2 * MP2::S) v |= (uint64_t)rq[(size_t)li * count];
-        if (li + 1 < 2 * MP2::S) v |= (uint64_t)rq[(size_t)(li + 1) * count] << MP2::W;
-        if (li + 2 < 2 * MP2::S) v |= (uint64_t)rq[(size_t)(li + 2) * count] << (2 * MP2::W);
-        tile[lane * TS + j] = (uint32_t)(v >> sh);
-      }
-    }
+  if (e0 >= count) return;  // whole wave past the end
+  const int64_t ec = e < count ? e : count - 1;  // tail lanes recompute the last element, store nothing
+  const int st = (int)count;
+  const uint32_t* rp = ws + ec;
+  const uint32_t* rq = ws + (size_t)2 * MP2::S4 * count + ec;
+  MP2 M;
+  M.init(Np2, key.p2.n0inv);
+  uint32_t b[MP2::L];
+  M.load_strided(b, rp, st);
+  M.add_sub_rows(b, key.p2x4_lim, rq, st);
+  M.mul(b, ARow{key.q2invR_p2});
+  M.reduce_once(b);  // t = (c_p - c_q) (q^2)^-1 mod p^2
+  uint64_t T[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) T[j] = rq[(size_t)j * st];  // + c_q
+  uint64_t acc = 0;
+  int nb = 0, w = 0;
+  auto flush = [&](int base) {
     wave_sync_mem_();
+#pragma unroll 4
     for (int r = 0; r < 32; ++r) {
       const int el = 2 * r + (lane >> 5), wd = lane & 31;
-      if (e0 + el < count) out[(size_t)(e0 + el) * nwords + c + wd] = tile[el * TS + wd];
+      if (e0 + el < count) out[(size_t)(e0 + el) * NW2 + (w - 32) + wd] = ring[el * RS + base + wd];
     }
     wave_sync_mem_();
+  };
+  auto emit = [&](uint32_t limb) {
+    acc |= (uint64_t)limb << nb;
+    nb += W;
+    if (nb >= 32 && w < NW2) {
+      ring[lane * RS + (w & 63)] = (uint32_t)acc;
+      acc >>= 32;
+      nb -= 32;
+      ++w;
+      if ((w & 31) == 0) flush((w - 32) & 63);
+    }
+  };
+  for (int i0 = 0; i0 < MP2::S4; i0 += 4) {
+    const uint4 a4 = ARow{key.q2_lim}.load4(i0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (i0 + r < S) {
+        const uint32_t ai = comp4(a4, r);
+        const uint64_t x0 = mad64(ai, b[0], T[0]);
+#pragma unroll
+        for (int j = 1; j < S; ++j) T[j - 1] = mad64(ai, b[j], T[j]);
+        T[S - 1] = 0;
+        T[0] += x0 >> W;
+        emit((uint32_t)x0 & MP2::MASK);
+      }
+    }
   }
+  uint32_t hi[S];
+  M.normalize(T, hi);
+#pragma unroll
+  for (int j = 0; j < S; ++j) emit(hi[j]);
 }
 
 // Raw encryption without obfuscation (paillier.py:283): c = 1 + n m  (m < n,
@@ -996,11 +1042,10 @@ __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* 
   M.mul(b, ARow{key.nR2_n2});
   M.add_row(b, key.n2.R1);
   const uint32_t* ae = a_words + (size_t)e * aw;
-  const int rows = 1 << key.win;
   for (int w = 0; w < key.nwin; ++w) {
-    int bit = w * key.win;
-    uint32_t d = digit_at(ae, aw, bit, key.win);
-    M.mul(b, ARowPacked<MN2::W, RW>{key.tab_n2 + ((size_t)w * rows + d) * RW});
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    M.mul(b, ARowPacked<MN2::W, RW>{key.tab_n2 + (size_t)(row0 + d) * RW});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
