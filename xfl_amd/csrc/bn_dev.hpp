@@ -25,6 +25,7 @@
 namespace xhe {
 
 #define XHE_DEV __device__ __forceinline__
+#define XHE_INL __attribute__((always_inline))  // on lambdas holding Montgomery products: a call would put T[] in scratch
 
 // Build switches (A/B measurement; defaults are the measured-best variant)
 #ifndef XHE_NPIPE
@@ -398,7 +399,7 @@ struct Mont {
     uint64_t xn = 0;
     uint32_t t = 0, mn = 0;
     int stage = 0;
-    auto advance = [&]() {
+    auto advance = [&]() XHE_INL {
       if (stage == 0) {
         T[0] += lead ? (x0 >> W) : 0ull;
         asm volatile("" : "+v"(T[0]));
@@ -466,7 +467,7 @@ struct Mont {
     uint64_t xn = 0;
     uint32_t t = 0, mn = 0;
     int stage = 0;
-    auto advance = [&]() {
+    auto advance = [&]() XHE_INL {
       // (the empty volatile asm pins each link between its barriers; plain
       // arithmetic would otherwise be sunk to its use at IR level)
       if (stage == 0) {

@@ -501,7 +501,7 @@ XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, c
   M.init(Np, md.n0inv);
   uint32_t b[MP2::L];
   const uint32_t* ae = a_words + (size_t)e * aw;
-  auto stage = [&](int w) {
+  auto stage = [&](int w) XHE_INL {
     int64_t row0;
     const uint32_t d = win_digit(key, ae, aw, w, row0);
     const uint32_t* row = tab + (size_t)(row0 + d) * RW;
@@ -631,7 +631,7 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc_w(KeyDev key, const uint32_t
   for (int j = 0; j < S; ++j) T[j] = rq[(size_t)j * st];  // + c_q
   uint64_t acc = 0;
   int nb = 0, w = 0;
-  auto flush = [&](int base) {
+  auto flush = [&](int base) XHE_INL {
     wave_sync_mem_();
 #pragma unroll 4
     for (int r = 0; r < 32; ++r) {
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc_w(KeyDev key, const uint32_t
     }
     wave_sync_mem_();
   };
-  auto emit = [&](uint32_t limb) {
+  auto emit = [&](uint32_t limb) XHE_INL {
     acc |= (uint64_t)limb << nb;
     nb += W;
     if (nb >= 32 && w < NW2) {
@@ -707,7 +707,7 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   // tab[t] = b^(2t+1), t < 16, then ~ebits squarings and ~ebits/6 products
   // (4-bit fixed windows: ebits/4).
   const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
-  auto square = [&]() {
+  auto square = [&]() XHE_INL {
     if (sq_lds) {
       const SqLds<MP2> L(sq_lds);
       L.put(b);
@@ -730,28 +730,41 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
     M.store_strided(b, tab + rs * t, st);
   }
   wave_sync_mem_();
-  bool first = true;
+  // The window schedule as one loop with one squaring and one product site
+  // (each site inlines a whole Montgomery product).
   int i = ebits - 1;
-#pragma unroll 1
-  while (i >= 0) {
-    if (!bit(i)) {
-      if (!first) square();
-      --i;
-      continue;
-    }
+  while (i >= 0 && !bit(i)) --i;
+  int pend_sq = 0, pend_mul = -1;
+  {  // first window: load its odd power
     int j = i - 4 < 0 ? 0 : i - 4;
-    while (!bit(j)) ++j;  // window [i..j] ends in a set bit
+    while (!bit(j)) ++j;
     uint32_t val = 0;
     for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
-    if (first) {
-      M.load_strided(b, tab + rs * (val >> 1), st);
-      first = false;
-    } else {
-#pragma unroll 1
-      for (int k = i; k >= j; --k) square();
-      M.mul(b, AStrided{tab + rs * (val >> 1), st});
-    }
+    M.load_strided(b, tab + rs * (val >> 1), st);
     i = j - 1;
+  }
+#pragma unroll 1
+  while (true) {
+    if (pend_sq > 0) {
+      square();
+      --pend_sq;
+    } else if (pend_mul >= 0) {
+      M.mul(b, AStrided{tab + rs * pend_mul, st});
+      pend_mul = -1;
+    } else if (i < 0) {
+      break;
+    } else if (!bit(i)) {
+      pend_sq = 1;
+      --i;
+    } else {
+      int j = i - 4 < 0 ? 0 : i - 4;
+      while (!bit(j)) ++j;  // window [i..j] ends in a set bit
+      uint32_t val = 0;
+      for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+      pend_sq = i - j + 1;
+      pend_mul = (int)(val >> 1);
+      i = j - 1;
+    }
   }
 }
 
