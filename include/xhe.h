@@ -153,6 +153,12 @@ int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int 
 int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
                     int64_t* count, int64_t* shape, int* ndim);
 
+/* Touch every page of a fresh host buffer from several threads (host only),
+ * so results copied in later do not take the first-touch faults on one
+ * thread; the bytes become zero. Used for the hundreds-of-MB ciphertext
+ * arrays of the drop-in (Paillier.encrypt's return, paillier.py:289-339). */
+int xhe_host_prefault(void* p, int64_t nbytes);
+
 /* Kernel timing: when enabled, the library brackets each launch of its
  * dominant kernels (k_djn_pow, k_dec_pow) with hipEvents on the launch stream.
  * xhe_profile(1) enables and clears, xhe_profile(0) disables and clears;

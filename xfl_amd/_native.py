@@ -62,6 +62,7 @@ SIGNATURES = {
                                        ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64), _vp, ctypes.POINTER(ctypes.c_int)]),
+    "xhe_host_prefault": (ctypes.c_int, [_vp, ctypes.c_int64]),
     "xhe_profile": (ctypes.c_int, [ctypes.c_int]),
     "xhe_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64)]),
@@ -154,10 +155,12 @@ def advise_huge(addr, nbytes):
 
 
 def empty(shape, dtype):
-    """np.empty for large host buffers the library writes into (hugepage-backed)."""
+    """np.empty for large host buffers the library writes into: hugepage-backed
+    and pre-faulted by the library's host threads (xhe_host_prefault)."""
     a = np.empty(shape, dtype=dtype)
     if a.nbytes >= (32 << 20):
         advise_huge(a.ctypes.data, a.nbytes)
+        lib().xhe_host_prefault(ctypes.c_void_p(a.ctypes.data), ctypes.c_int64(a.nbytes))
     return a
 
 

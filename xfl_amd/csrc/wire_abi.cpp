@@ -39,6 +39,21 @@ int xhe_fail(int code, const std::string& msg) {
 
 extern "C" {
 
+int xhe_host_prefault(void* p, int64_t nbytes) {
+  // One write per 4 KiB page, the range split over the codec threads: the
+  // kernel's zero-fill of fresh pages then runs on all of them instead of
+  // inside the single thread that later copies device results in.
+  if (!p || nbytes < 0) return xhe_fail(XHE_EINVAL, "xhe_host_prefault: bad argument");
+  const int T = nbytes >= (64 << 20) ? codec_threads() : 1;
+  auto* base = static_cast<volatile uint8_t*>(p);
+  const int64_t per = ((nbytes + T - 1) / T + 4095) & ~(int64_t)4095;
+  xhe::wire::run_parallel(T, [&](int t) {
+    const int64_t lo = (int64_t)t * per, hi = std::min<int64_t>(nbytes, lo + per);
+    for (int64_t o = lo; o < hi; o += 4096) base[o] = 0;
+  });
+  return XHE_OK;
+}
+
 int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
                     uint8_t* out, int64_t cap, int64_t* out_len) {
   return guarded([&]() -> int {

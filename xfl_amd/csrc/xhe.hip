@@ -82,14 +82,20 @@ struct Shape8192 {
   using MN2X = Mont<640, 26, 16>;
 };
 
-// XHE_ONLY_2048: a development build with the 2048-bit shapes only (a
-// fraction of the compile time, for kernel A/B runs through $XHE_LIB); the
-// shipped library has every key size.
-#ifdef XHE_ONLY_2048
-constexpr bool key_bits_supported(int K) { return K == 2048; }
+// XHE_ONLY_BITS=K (XHE_ONLY_2048 = 2048): a development build with one key
+// size's shapes only (a fraction of the compile time, for kernel A/B runs
+// through $XHE_LIB); the shipped library has every key size.
+#if defined(XHE_ONLY_2048) && !defined(XHE_ONLY_BITS)
+#define XHE_ONLY_BITS 2048
+#endif
+#ifdef XHE_ONLY_BITS
+constexpr bool key_bits_supported(int K) { return K == XHE_ONLY_BITS; }
 template <class F>
 decltype(auto) with_shape(int, F&& f) {
-  return f(Shape2048{});
+  if constexpr (XHE_ONLY_BITS == 2048) return f(Shape2048{});
+  else if constexpr (XHE_ONLY_BITS == 3072) return f(Shape3072{});
+  else if constexpr (XHE_ONLY_BITS == 4096) return f(Shape4096{});
+  else return f(Shape8192{});
 }
 #else
 constexpr bool key_bits_supported(int K) { return K == 2048 || K == 3072 || K == 4096 || K == 8192; }
