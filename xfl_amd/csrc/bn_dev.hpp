@@ -46,6 +46,9 @@ namespace xhe {
 #ifndef XHE_M_MAD
 #define XHE_M_MAD 0  // Montgomery digit m = x0 * n0inv by v_mad_u64_u32 instead of v_mul_lo_u32
 #endif
+#ifndef XHE_SQ_ACC
+#define XHE_SQ_ACC 2  // partial sums per column of Mont::sqr's product scan
+#endif
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif
@@ -450,6 +453,167 @@ struct Mont {
     T[L - 1] = 0;
     x0 = xn;
     m = mn;
+  }
+
+  // ---- squaring (TPI == 1): the square by product scanning, then one
+  // Montgomery reduction. Reduction-only blocks: T[j-1+k] = T[j+k] + m*N[j+k].
+  XHE_DEV void red4v(uint64_t (&T)[L], uint32_t m, int j, const uint32_t* n) const {
+    asm("v_mad_u64_u32 %0, vcc, %5, %6, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %5, %7, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %5, %8, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %5, %9, %4"
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2])
+        : "v"(T[j + 3]), "v"(m), "s"(n[0]), "s"(n[1]), "s"(n[2]), "s"(n[3])
+        : "vcc");
+  }
+  XHE_DEV void red8v(uint64_t (&T)[L], uint32_t m, int j, const uint32_t* n) const {
+    asm("v_mad_u64_u32 %0, vcc, %9, %10, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %9, %11, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %9, %12, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %9, %13, %4\n\t"
+        "v_mad_u64_u32 %4, vcc, %9, %14, %5\n\t"
+        "v_mad_u64_u32 %5, vcc, %9, %15, %6\n\t"
+        "v_mad_u64_u32 %6, vcc, %9, %16, %7\n\t"
+        "v_mad_u64_u32 %7, vcc, %9, %17, %8"
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4]),
+          "+v"(T[j + 5]), "+v"(T[j + 6])
+        : "v"(T[j + 7]), "v"(m), "s"(n[0]), "s"(n[1]), "s"(n[2]), "s"(n[3]), "s"(n[4]), "s"(n[5]), "s"(n[6]),
+          "s"(n[7])
+        : "vcc");
+  }
+  // One reduction row: T <- (T + m*N) / 2^W with limb `hi_i` of the square's
+  // upper half entering at the top; the same schedule as step1 (modulus limbs
+  // one block ahead, the next row's digit formed under the first blocks).
+  XHE_DEV void step1_red(const uint32_t* Np, const NRes& R, uint64_t (&T)[L], uint32_t hi_i, uint32_t& m,
+                         uint64_t& x0) const {
+    uint64_t xn = 0;
+    uint32_t t = 0, mn = 0;
+    int stage = 0;
+    auto advance = [&]() XHE_INL {
+      if (stage == 0) {
+        T[0] += x0 >> W;
+        asm volatile("" : "+v"(T[0]));
+      } else if (stage == 1) {
+        xn = T[0];
+      } else if (stage == 2) {
+        t = (uint32_t)xn * n0inv;
+        asm volatile("" : "+v"(t));
+      } else if (stage == 3) {
+        mn = t & MASK;
+        asm volatile("" : "+v"(mn));
+      }
+      ++stage;
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    uint32_t nb[2][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nb[0][k] = R.f[k];
+    x0 = mad64s(m, R.n0, x0);
+    red4v(T, m, 1, R.h);
+    advance();
+#pragma unroll
+    for (int blk = 0; blk < (J8 - 5) / 8; ++blk) {
+      const int j = 5 + 8 * blk;
+      const int cur = blk & 1;
+      if (j + 16 <= J8) {
+        asm volatile("" ::"s"(nb[cur][0]), "s"(nb[cur][1]), "s"(nb[cur][2]), "s"(nb[cur][3]), "s"(nb[cur][4]),
+                     "s"(nb[cur][5]), "s"(nb[cur][6]), "s"(nb[cur][7]));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nb[cur ^ 1][k] = Np[j + 8 + k];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      red8v(T, m, j, nb[cur]);
+      if (stage < 4) advance();
+      else __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (TL >= 4) red4v(T, m, J8, R.t);
+#pragma unroll
+    for (int k = (TL >= 4 ? 4 : 0); k < TL; ++k) T[J8 + k - 1] = mad64s(m, R.t[k], T[J8 + k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (stage < 4) advance();
+    T[L - 1] = hi_i;
+    x0 = xn;
+    m = mn;
+  }
+  // Column C of the square into a 64-bit sum: 2 * sum_{i < C-i} a_i a_{C-i}
+  // (+ a_{C/2}^2 for even C) + carry; XHE_SQ_ACC partial sums break the mad
+  // chain.
+  template <int C>
+  XHE_DEV uint64_t sq_column(const uint32_t (&a)[L], uint64_t carry) const {
+    constexpr int lo = C - (S - 1) > 0 ? C - (S - 1) : 0;
+    uint64_t s[XHE_SQ_ACC] = {};
+#pragma unroll
+    for (int i = lo; 2 * i < C; ++i) s[(i - lo) % XHE_SQ_ACC] = mad64(a[i], a[C - i], s[(i - lo) % XHE_SQ_ACC]);
+#pragma unroll
+    for (int k = 1; k < XHE_SQ_ACC; ++k) s[0] += s[k];
+    uint64_t x = (s[0] << 1) + carry;
+    if constexpr ((C & 1) == 0) x = mad64(a[C / 2], a[C / 2], x);
+    return x;
+  }
+  template <int C, class HI>
+  XHE_DEV void sq_columns(const uint32_t (&a)[L], uint32_t (&lo)[L], uint64_t carry, uint4& q, const HI& hi) const {
+    if constexpr (C < 2 * S) {
+      const uint64_t x = C < 2 * S - 1 ? sq_column<C < 2 * S - 1 ? C : 0>(a, carry) : carry;
+      const uint32_t limb = (uint32_t)x & MASK;
+      if constexpr (C < S) {
+        lo[C] = limb;
+      } else {
+        constexpr int h = C - S;
+        if constexpr ((h & 3) == 0) q.x = limb;
+        else if constexpr ((h & 3) == 1) q.y = limb;
+        else if constexpr ((h & 3) == 2) q.z = limb;
+        else q.w = limb;
+        if constexpr ((h & 3) == 3 || C == 2 * S - 1) {
+          if constexpr ((h & 3) < 3) q.w = 0;
+          if constexpr ((h & 3) < 2) q.z = 0;
+          if constexpr ((h & 3) < 1) q.y = 0;
+          hi.put4(h >> 2, q);
+        }
+      }
+      sq_columns<C + 1, HI>(a, lo, x >> W, q, hi);
+    }
+  }
+  // b <- b^2 R^-1 mod N (TPI == 1 shapes with the SGPR modulus pipeline; others
+  // fall back to mul with `a` = a copy of b). The square's S(S+1)/2 column
+  // products replace the S^2 a_i*b_k mads of a general product; its upper S
+  // limbs go through `hi` (the caller's per-lane LDS slot: put4 / load4) into
+  // the reduction. Bounds: a column sum is below (S/2+1) 2^(2W+1) + carry; the
+  // reduction adds S terms below 2^(2W) to limbs below 2^W - as in mul().
+  static constexpr bool kSqr = TPI == 1 && L >= 13 && XHE_NPIPE;
+  template <class HI>
+  XHE_DEV void sqr(uint32_t (&b)[L], const HI& hi) const {
+    uint32_t lo[L];
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    sq_columns<0, HI>(b, lo, 0ull, q, hi);
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = lo[j];
+    hi.sync();
+    const uint32_t* Np = np();
+    NRes R;
+    load_res(Np, R);
+    uint64_t x0 = T[0];
+    uint32_t m = ((uint32_t)x0 * n0inv) & MASK;
+    uint4 cur = hi.load4(0);
+    int i = 0;
+    for (; i + 4 <= S; i += 4) {
+      uint4 nxt = hi.load4(i + 4 < S4 ? i + 4 : i);
+      __builtin_amdgcn_sched_barrier(0);
+      step1_red(Np, R, T, cur.x, m, x0);
+      __builtin_amdgcn_sched_barrier(0);
+      step1_red(Np, R, T, cur.y, m, x0);
+      __builtin_amdgcn_sched_barrier(0);
+      step1_red(Np, R, T, cur.z, m, x0);
+      __builtin_amdgcn_sched_barrier(0);
+      step1_red(Np, R, T, cur.w, m, x0);
+      __builtin_amdgcn_sched_barrier(0);
+      cur = nxt;
+    }
+#pragma unroll
+    for (int r = 0; r < (S & 3); ++r) step1_red(Np, R, T, comp4(cur, r), m, x0);
+    normalize(T, b);
   }
 
   // One column of the product: T <- (T + a_i*b + m*N) / 2^W, software-

@@ -435,6 +435,9 @@ struct SqLds {
     if constexpr (M_::TPI == 1) return *reinterpret_cast<const uint4*>(slot + (i >> 2) * 256);
     else return *reinterpret_cast<const uint4*>(slot + i);
   }
+  // quad-wise writes (Mont::sqr's upper half, TPI == 1), then sync() before reading
+  XHE_DEV void put4(int q, const uint4& v) const { *reinterpret_cast<uint4*>(slot + q * 256) = v; }
+  XHE_DEV void sync() const { wave_sync_mem_(); }
 };
 
 
@@ -708,6 +711,12 @@ XHE_DEV void pow_uniform_exp(const MP2& M, uint32_t (&b)[MP2::L], const uint32_t
   // (4-bit fixed windows: ebits/4).
   const size_t rs = (size_t)MP2::S4 * st;  // row stride in words
   auto square = [&]() XHE_INL {
+    if constexpr (MP2::kSqr) {
+      if (sq_lds) {  // the slot carries the square's upper half into the reduction
+        M.sqr(b, SqLds<MP2>(sq_lds));
+        return;
+      }
+    }
     if (sq_lds) {
       const SqLds<MP2> L(sq_lds);
       L.put(b);
