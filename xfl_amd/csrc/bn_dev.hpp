@@ -46,6 +46,9 @@ namespace xhe {
 #ifndef XHE_M_MAD
 #define XHE_M_MAD 0  // Montgomery digit m = x0 * n0inv by v_mad_u64_u32 instead of v_mul_lo_u32
 #endif
+#ifndef XHE_PQ_PAIR
+#define XHE_PQ_PAIR 0  // 1: DJN tables with p^2/q^2 rows of one (window, digit) adjacent and k_djn_pow_lds pairing p/q blocks per XCD (A/B: no gain)
+#endif
 #ifndef XHE_SQ_ACC
 #define XHE_SQ_ACC 2  // partial sums per column of Mont::sqr's product scan
 #endif

@@ -232,7 +232,7 @@ void build_tables_sync(xhe_key* k, const ModDev* md, const uint32_t* const* d_hM
 // low entry.
 template <class MP2, int RW>
 void build_tables_seg(const ModDev& md, const uint32_t* d_base, int win, int nwin, int nbases, uint32_t* d_tab,
-                      uint32_t* d_chain, uint32_t* d_ws, hipStream_t s) {
+                      int64_t rs, uint32_t* d_chain, uint32_t* d_ws, hipStream_t s) {
   const int half = win / 2;
   hipLaunchKernelGGL(k_tab_bases<MP2>, dim3(1), dim3(64), 0, s, md, d_base, win, nbases, d_chain, d_ws);
   HIPCHK(hipGetLastError());
@@ -251,7 +251,8 @@ void build_tables_seg(const ModDev& md, const uint32_t* d_base, int win, int nwi
     HIPCHK(hipGetLastError());
   }
   int64_t rows = (int64_t)nwin << win;
-  hipLaunchKernelGGL((k_tab_combine<MP2, RW>), blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_chain, d_tab);
+  hipLaunchKernelGGL((k_tab_combine<MP2, RW>), blocks(rows), dim3(256), 0, s, md, md.N, win, nwin, d_chain, d_tab,
+                     rs);
   HIPCHK(hipGetLastError());
 }
 
@@ -262,16 +263,17 @@ template <class MP2, int RW>
 void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t* d_tab, uint32_t* d_chain,
                     uint32_t* d_ws, hipStream_t s) {
   const int win = k->kd.win, nwin = k->kd.nwin, nhi = k->kd.nhi;
+  const int64_t rs = RW == k->K / 32 ? k->kd.tab_rs : RW;  // p^2/q^2 rows (maybe interleaved) or n^2 rows
   if (nhi == 0) {
-    build_tables_seg<MP2, RW>(md, d_hM, win, nwin, nwin, d_tab, d_chain, d_ws, s);
+    build_tables_seg<MP2, RW>(md, d_hM, win, nwin, nwin, d_tab, rs, d_chain, d_ws, s);
     return;
   }
   uint32_t* base2 = d_ws + 2 * MP2::S4;  // d_ws rows: 0 = squaring scratch, 2 = the narrow windows' base
-  build_tables_seg<MP2, RW>(md, d_hM, win + 1, nhi, nhi + 1, d_tab, d_chain, d_ws, s);
+  build_tables_seg<MP2, RW>(md, d_hM, win + 1, nhi, nhi + 1, d_tab, rs, d_chain, d_ws, s);
   HIPCHK(hipMemcpyAsync(base2, d_chain + ((size_t)nhi * chain_rows_h(win + 1) + 1) * MP2::S4,
                         MP2::S4 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  build_tables_seg<MP2, RW>(md, base2, win, nwin - nhi, nwin - nhi, d_tab + ((size_t)nhi << (win + 1)) * RW, d_chain,
-                            d_ws, s);
+  build_tables_seg<MP2, RW>(md, base2, win, nwin - nhi, nwin - nhi, d_tab + ((size_t)nhi << (win + 1)) * rs, rs,
+                            d_chain, d_ws, s);
 }
 
 ModDev moddev(uint32_t* base, const ModOff& o) {
@@ -457,11 +459,18 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       size_t rows = (size_t)(kd.nwin + kd.nhi) << kd.win;
       size_t tab_words = rows * (size_t)(K / 32);  // packed rows: Shape::RW = K/32 words (p^2 < 2^K)
       HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
+#if XHE_PQ_PAIR
+      kd.tab_rs = 2 * (K / 32);  // rows (w, d) of p^2 and q^2 side by side
+      kd.tab_p2 = k->d_tab;
+      kd.tab_q2 = k->d_tab + K / 32;
+#else
+      kd.tab_rs = K / 32;
       kd.tab_p2 = k->d_tab;
       kd.tab_q2 = k->d_tab + tab_words;
+#endif
       const ModDev mds[2] = {kd.p2, kd.q2};
       const uint32_t* hms[2] = {B + o.hM_p2, B + o.hM_q2};
-      uint32_t* tabs[2] = {k->d_tab, k->d_tab + tab_words};
+      uint32_t* tabs[2] = {const_cast<uint32_t*>(kd.tab_p2), const_cast<uint32_t*>(kd.tab_q2)};
       with_shape(K, [&](auto sh) {
         using Sh = decltype(sh);
         build_tables_sync<typename Sh::MP2, Sh::RW>(k, mds, hms, tabs, 2);
@@ -571,7 +580,12 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
       ProfScope ps("k_djn_pow", s);
 #if XHE_LDS_ROWS
       if constexpr (MP2::TPI == 1) {
-        hipLaunchKernelGGL((k_djn_pow_lds<MP2, Sh::RW>), dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
+#if XHE_PQ_PAIR
+        const dim3 grid((unsigned)(16 * ((n + 1023) / 1024)));  // 8 chunks of 128 elements x 2 primes per 16 blocks
+#else
+        const dim3 grid((unsigned)((n + 127) / 128), 2);
+#endif
+        hipLaunchKernelGGL((k_djn_pow_lds<MP2, Sh::RW>), grid, dim3(128), 0, s, k->kd,
                            k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
                            k->rand_words, n, ws);
       } else

@@ -54,8 +54,9 @@ struct KeyDev {
   const uint32_t* q2invR_p2;  // (q^2)^-1 * R mod p^2
   const uint32_t* q2_lim;     // q^2 (MP2 limbs)
   const uint32_t* p2x4_lim;   // 4 p^2 (MP2 limbs)
-  const uint32_t* tab_p2;     // h^(d*2^bit(w)) * R mod p^2, packed rows, windows as win_loc()
-  const uint32_t* tab_q2;
+  const uint32_t* tab_p2;     // h^(d*2^bit(w)) * R mod p^2, packed rows, windows as win_digit()
+  const uint32_t* tab_q2;     // (XHE_PQ_PAIR: interleaved with tab_p2, row (w, d) of q^2 right after p^2's)
+  int64_t tab_rs;             // words from one row of tab_p2 / tab_q2 to the next
   int win, nwin, nhi;         // nhi: the first nhi windows are win+1 bits wide (0: uniform)
   // ---- mod p / q (shape MP), decrypt
   ModDev p, q;
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow(KeyDev key, const uint32_t* 
   for (int w = 0; w < key.nwin; ++w) {
     int64_t row0;
     const uint32_t d = win_digit(key, ae, aw, w, row0);
-    M.mul(b, ARowPacked<MP2::W, RW>{tab + (size_t)(row0 + d) * RW});
+    M.mul(b, ARowPacked<MP2::W, RW>{tab + (size_t)(row0 + d) * key.tab_rs});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -466,7 +467,7 @@ __global__ void __launch_bounds__(256, 2) k_djn_pow_x(KeyDev key, const uint32_t
   for (int w = 0; w < key.nwin; ++w) {
     int64_t row0;
     const uint32_t d = win_digit(key, ae, aw, w, row0);
-    M.mul(b, ARowPacked<MX::W, RW>{tab + (size_t)(row0 + d) * RW});
+    M.mul(b, ARowPacked<MX::W, RW>{tab + (size_t)(row0 + d) * key.tab_rs});
   }
   M.mul(b, AOne{});
   M.reduce_once(b);
@@ -507,7 +508,7 @@ XHE_DEV void djn_prime_lds(const KeyDev& key, const uint32_t* __restrict__ Np, c
   auto stage = [&](int w) XHE_INL {
     int64_t row0;
     const uint32_t d = win_digit(key, ae, aw, w, row0);
-    const uint32_t* row = tab + (size_t)(row0 + d) * RW;
+    const uint32_t* row = tab + (size_t)(row0 + d) * key.tab_rs;
 #pragma unroll
     for (int k = 0; k < RW / 4; ++k)
       __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
@@ -558,8 +559,20 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
                                                         uint32_t* __restrict__ ws) {
   static_assert(MP2::TPI == 1, "LDS row staging is per lane");
   __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
+#if XHE_PQ_PAIR
+  // 1-D grid: block b runs on XCD b % 8 (round-robin dispatch; for speed
+  // only, correctness does not depend on it); of each XCD's consecutive
+  // blocks, two take the same element block for p^2 and q^2, so both read
+  // the same (window, digit) row pair - one TLB entry and one DRAM page -
+  // at about the same time on the same L2.
+  const int64_t bid = blockIdx.x, j = bid >> 3;
+  const int prime = (int)(j & 1);
+  const int64_t chunk = ((j >> 1) << 3) | (bid & 7);
+  const int64_t e = chunk * blockDim.x + threadIdx.x;
+#else
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int prime = blockIdx.y;
+#endif
   uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
   if (e >= count) return;
   djn_prime_lds<MP2, RW>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
@@ -1469,7 +1482,7 @@ __global__ void __launch_bounds__(256, 2) k_tab_level(ModDev md, const uint32_t*
 template <class MP2, int RW>
 __global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, const uint32_t* __restrict__ Nm, int win,
                                                          int nwin, const uint32_t* __restrict__ chain,
-                                                         uint32_t* __restrict__ tab) {
+                                                         uint32_t* __restrict__ tab, int64_t rs) {
   __shared__ __attribute__((aligned(16))) uint32_t sc_all[(256 / MP2::TPI) * MP2::S4];
   const int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
   const int64_t rows = (int64_t)nwin << win;
@@ -1494,7 +1507,7 @@ __global__ void __launch_bounds__(256, 2) k_tab_combine(ModDev md, const uint32_
   uint32_t* sc = sc_all + (size_t)((threadIdx.x % 256) / MP2::TPI) * MP2::S4;
   M.store_row(b, sc);
   wave_sync_mem_();
-  pack_words_<MP2::W, MP2::TPI>(sc, 1, MP2::S, tab + (size_t)idx * RW, RW);
+  pack_words_<MP2::W, MP2::TPI>(sc, 1, MP2::S, tab + (size_t)idx * rs, RW);
 }
 
 // Montgomery product of two rows (host-side setup helper / unit tests):
