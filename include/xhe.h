@@ -153,6 +153,23 @@ int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int 
 int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
                     int64_t* count, int64_t* shape, int* ndim);
 
+/* A zstd frame (RFC 8878, one frame, content size in the header) holding
+ * src[0..n) as raw blocks, written by several host threads: what
+ * Paillier.serialize(compression=True) sends for large arrays
+ * (paillier.py:244-258 zstd.compress). Ciphertext bytes are incompressible
+ * (zstd level 3 keeps 98 % of a pickled ciphertext array), so the frame
+ * costs a parallel copy instead of a single-threaded entropy search, and any
+ * zstd decoder (the reference's zstd.decompress) reads it back. *out_len =
+ * the frame's size (xhe_zstd_raw_frame_size(n)); XHE_EOVERFLOW when cap is
+ * smaller (dst may be NULL). */
+int64_t xhe_zstd_raw_frame_size(int64_t n);
+int xhe_zstd_raw_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len);
+/* Its inverse for frames made only of raw blocks, copied out in parallel
+ * (ciphertext_from(compression=True), paillier.py:260-264): *out_len = the
+ * content size; XHE_ENOTSUP for any other frame (the caller then uses
+ * libzstd), XHE_EOVERFLOW when cap is too small. */
+int xhe_zstd_raw_extract(const uint8_t* src, int64_t len, uint8_t* dst, int64_t cap, int64_t* out_len);
+
 /* Touch every page of a fresh host buffer from several threads (host only),
  * so results copied in later do not take the first-touch faults on one
  * thread; the bytes become zero. Used for the hundreds-of-MB ciphertext

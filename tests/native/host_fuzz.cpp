@@ -10,6 +10,12 @@
 //                            encode -> decode round trips of random vectors.
 //                            A malformed input may only raise (runtime_error);
 //                            any memory or UB error aborts under the sanitizers.
+//   host_fuzz zstd           xhe_zstd_raw_frame / xhe_zstd_raw_extract (wire_abi.cpp,
+//                            the framing of Paillier.serialize(compression=True)
+//                            and the fast path of ciphertext_from): round trips
+//                            at block-boundary sizes, then every truncation,
+//                            header and block-header corruption and random
+//                            flips of small frames; extract may only refuse.
 //   host_fuzz bn             hostbn.hpp arithmetic (key setup, context.py:28-71)
 //                            on lines "op a b m" (hex) from stdin, results to
 //                            stdout for the Python side to check against int.
@@ -22,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/xhe.h"
 #include "../../xfl_amd/csrc/hostbn.hpp"
 #include "../../xfl_amd/csrc/wire.hpp"
 
@@ -224,8 +231,55 @@ static int bn_mode() {
   return 0;
 }
 
+static int zstd_mode() {
+  std::mt19937_64 rng(777);
+  long frames = 0, refused = 0;
+  const int64_t B = 1 << 17;
+  const int64_t sizes[] = {0, 1, 2, 1000, B - 1, B, B + 1, 3 * B, 5 * B + 17, (8 << 20) + 3};
+  auto extract = [&](const Bytes& f, int64_t cap) -> int {
+    int64_t n = 0;
+    Bytes out((size_t)std::max<int64_t>(cap, 1));
+    int rc = xhe_zstd_raw_extract(f.empty() ? nullptr : f.data(), (int64_t)f.size(), cap ? out.data() : nullptr, cap,
+                                  &n);
+    if (rc != XHE_OK && rc != XHE_ENOTSUP && rc != XHE_EOVERFLOW && rc != XHE_EINVAL) std::abort();
+    if (rc != XHE_OK) ++refused;
+    return rc;
+  };
+  for (int64_t n : sizes) {
+    Bytes src((size_t)n);
+    for (auto& b : src) b = (uint8_t)rng();
+    const int64_t size = xhe_zstd_raw_frame_size(n);
+    Bytes f((size_t)size);
+    int64_t got = 0;
+    if (xhe_zstd_raw_frame(n ? src.data() : nullptr, n, f.data(), size, &got) != XHE_OK || got != size) std::abort();
+    if (xhe_zstd_raw_frame(n ? src.data() : nullptr, n, f.data(), size - 1, &got) != XHE_EOVERFLOW) std::abort();
+    ++frames;
+    Bytes back((size_t)std::max<int64_t>(n, 1));
+    int64_t m = -1;
+    if (xhe_zstd_raw_extract(f.data(), size, back.data(), n, &m) != XHE_OK || m != n) std::abort();
+    if (n && std::memcmp(back.data(), src.data(), (size_t)n)) std::abort();
+    if (n > 4 * B) continue;  // mutate the small frames only
+    for (int64_t k = 0; k < size; k += (k < 64 ? 1 : 997)) extract(Bytes(f.begin(), f.begin() + k), n);
+    for (int64_t pos = 0; pos < std::min<int64_t>(size, 32); ++pos)
+      for (int v : {0x00, 0x01, 0x04, 0x20, 0x40, 0x80, 0xC0, 0xFF}) {
+        Bytes g = f;
+        g[pos] = (uint8_t)v;
+        extract(g, n);
+        extract(g, n + 4096);
+      }
+    for (int t = 0; t < 300; ++t) {
+      Bytes g = f;
+      g[rng() % g.size()] = (uint8_t)rng();
+      extract(g, n);
+    }
+  }
+  std::printf("zstd frames %ld refused %ld\n", frames, refused);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "bn") return bn_mode();
+  if (argc >= 2 && std::string(argv[1]) == "zstd") return zstd_mode();
   if (argc < 3 || std::string(argv[1]) != "wire") {
     std::fprintf(stderr, "usage: host_fuzz wire SEED... | host_fuzz bn < cases\n");
     return 2;

@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from tests.conftest import FIXTURES, hx, load_fixture
+from tests.conftest import FIXTURES, ROOT, hx, load_fixture
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
@@ -27,8 +27,8 @@ SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-f
 @pytest.fixture(scope="module")
 def harness(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("hostfuzz") / "host_fuzz")
-    subprocess.run(["g++", "-O1", "-g", "-std=c++17", *SAN, os.path.join(HERE, "native", "host_fuzz.cpp"),
-                    "-o", exe], check=True)
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", *SAN, os.path.join(HERE, "native", "host_fuzz.cpp"),
+                    os.path.join(ROOT, "xfl_amd", "csrc", "wire_abi.cpp"), "-o", exe], check=True)
     return exe
 
 
@@ -70,6 +70,13 @@ def test_wire_decoder_fuzz_under_sanitizers(harness, tmp_path):
     assert r.stdout.startswith(f"seeds {len(seeds)} "), r.stdout
     rejected = int(r.stdout.split()[-1])
     assert rejected > 1000  # the mutants were exercised, not silently accepted
+
+
+def test_zstd_raw_frames_under_sanitizers(harness):
+    r = subprocess.run([harness, "zstd"], capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    frames, refused = int(r.stdout.split()[2]), int(r.stdout.split()[4])
+    assert frames == 10 and refused > 1000, r.stdout
 
 
 def test_hostbn_under_sanitizers(harness):

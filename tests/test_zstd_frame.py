@@ -1,0 +1,92 @@
+"""The zstd framing of Paillier.serialize(compression=True) (paillier.py:244-271):
+large payloads become one frame of raw blocks (xhe_zstd_raw_frame), which the
+system libzstd - the decoder the reference's zstd.decompress wraps - must read
+back bit-exactly; small ones stay libzstd level-3 frames. Host only (CPU)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from xfl_amd import _native as nat
+from xfl_amd import compat
+
+BLOCK = 1 << 17
+
+
+def libzstd_decompress(frame):
+    L = compat._lib()
+    size = L.ZSTD_getFrameContentSize(frame, len(frame))
+    assert size < (1 << 63), "frame must carry its content size"
+    dst = ctypes.create_string_buffer(max(int(size), 1))
+    n = L.ZSTD_decompress(dst, int(size), frame, len(frame))
+    assert not L.ZSTD_isError(n), "libzstd rejected the frame"
+    return dst.raw[:n]
+
+
+@pytest.mark.parametrize("n", [compat.RAW_FRAME_MIN, 8 * BLOCK + 1, 64 * BLOCK, (9 << 20) + 12345])
+def test_raw_frame_reads_back_through_libzstd(n):
+    data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+    frame = compat.compress(data)
+    assert len(frame) == nat.lib().xhe_zstd_raw_frame_size(n) == 14 + n + 3 * (-(-n // BLOCK))
+    assert frame[:4] == b"\x28\xb5\x2f\xfd"
+    assert libzstd_decompress(frame) == data      # any zstd decoder
+    assert compat.decompress(frame) == data       # the parallel raw path
+    assert compat._raw_extract(frame) == data
+
+
+def test_small_payloads_stay_libzstd_frames():
+    data = b"RawCiphertext" * 1000
+    frame = compat.compress(data)
+    assert len(frame) < len(data) // 10           # really compressed
+    assert compat._raw_extract(frame) is None      # not raw blocks: libzstd path
+    assert compat.decompress(frame) == data
+
+
+def test_libzstd_frames_take_the_libzstd_path():
+    data = (b"\x00" * 100 + bytes(range(256))) * 8000   # > RAW_FRAME_MIN, compressible
+    L = compat._lib()
+    cap = L.ZSTD_compressBound(len(data))
+    dst = ctypes.create_string_buffer(cap)
+    k = L.ZSTD_compress(dst, cap, data, len(data), 3)
+    frame = dst.raw[:k]
+    assert compat._raw_extract(frame) is None
+    assert compat.decompress(frame) == data
+
+
+def test_raw_extract_rejects_damaged_frames():
+    data = np.random.default_rng(1).integers(0, 256, 3 * BLOCK + 7, dtype=np.uint8).tobytes()
+    frame = bytearray(compat.compress(data))
+    L = nat.lib()
+    n = ctypes.c_int64()
+    for bad in (frame[:-1], frame + b"\x00", frame[:20]):
+        bad = bytes(bad)
+        assert L.xhe_zstd_raw_extract(bad, len(bad), None, 0, ctypes.byref(n)) == nat.XHE_ENOTSUP
+    wrong_size = bytearray(frame)
+    wrong_size[6] ^= 1                             # content size no longer matches the blocks
+    wrong_size = bytes(wrong_size)
+    assert L.xhe_zstd_raw_extract(wrong_size, len(wrong_size), None, 0, ctypes.byref(n)) == nat.XHE_ENOTSUP
+    checksum = bytearray(frame)
+    checksum[4] |= 0x04                            # content checksum flag: left to libzstd
+    checksum = bytes(checksum)
+    assert L.xhe_zstd_raw_extract(checksum, len(checksum), None, 0, ctypes.byref(n)) == nat.XHE_ENOTSUP
+    good = bytes(frame)
+    assert L.xhe_zstd_raw_extract(good, len(good), None, 0, ctypes.byref(n)) == nat.XHE_EOVERFLOW
+    assert n.value == len(data)
+
+
+def test_serialize_compressed_roundtrip_large_array():
+    """Paillier.serialize(compression=True) of a ciphertext array above the
+    threshold -> ciphertext_from(compression=True) gives the same words."""
+    from xfl_amd.paillier import Paillier
+    from xfl_amd.paillier.array import PaillierArray
+    count, n2w = 4096, 128
+    w = np.random.default_rng(2).integers(0, 1 << 32, (count, n2w), dtype=np.uint64).astype(np.uint32)
+    w[:, -1] &= 0x7FFFFFFF
+    e = np.random.default_rng(3).integers(-60, 0, count).astype(np.int32)
+    arr = PaillierArray.from_buffers(None, w, e, (count,))
+    blob = Paillier.serialize(arr, compression=True)
+    assert len(blob) > compat.RAW_FRAME_MIN
+    plain = libzstd_decompress(blob)
+    assert plain == Paillier.serialize(arr, compression=False)
+    back = Paillier.ciphertext_from(None, blob, compression=True)
+    assert np.array_equal(back.words, w) and np.array_equal(back.exponents, e)

@@ -7,8 +7,13 @@
   required here — `loads` maps that global to a decoder of gmpy2's binary
   format (b'\\x01' + sign byte + little-endian magnitude). Values we emit are
   Python ints, which the reference's gmpy2 arithmetic accepts unchanged.
-* `compression=True` is zstd (the reference's `zstd.compress`), implemented
-  with the system libzstd through ctypes (standard frames, level 3).
+* `compression=True` is zstd (the reference's `zstd.compress`): one standard
+  frame with the content size in its header, which the reference's
+  `zstd.decompress` reads. Payloads below 1 MiB are compressed by the system
+  libzstd (level 3, through ctypes); larger ones - ciphertext arrays, of
+  which level 3 keeps 98 % - are framed as raw blocks by the library's host
+  threads (`xhe_zstd_raw_frame`), and such frames are read back by a
+  parallel copy.
 """
 import ctypes
 import ctypes.util
@@ -121,9 +126,25 @@ def _dst(cap):
     return buf
 
 
+RAW_FRAME_MIN = 1 << 20  # payloads from this size up are framed as raw blocks
+
+
 def compress(data: bytes, level: int = 3) -> bytes:
     """zstd frame of data (the reference's zstd.compress, paillier.py:244-258):
-    one frame, content size in the header."""
+    one frame, content size in the header. Payloads of RAW_FRAME_MIN bytes
+    and more - ciphertext arrays, 98 % incompressible at level 3 - become one
+    frame of raw blocks written by the library's host threads
+    (xhe_zstd_raw_frame); smaller ones are compressed by libzstd."""
+    if len(data) >= RAW_FRAME_MIN:
+        from . import _native as nat
+        L = nat.lib()
+        size = L.xhe_zstd_raw_frame_size(len(data))
+        out = bytes(size)  # written in place; nothing else references it yet
+        ptr = ctypes.cast(out, ctypes.c_void_p)
+        nat.advise_huge(ptr.value, size)
+        n = ctypes.c_int64()
+        nat.check(L.xhe_zstd_raw_frame(data, len(data), ptr, size, ctypes.byref(n)), "zstd frame")
+        return out
     L = _lib()
     cap = L.ZSTD_compressBound(len(data))
     dst = _dst(cap)
@@ -133,7 +154,28 @@ def compress(data: bytes, level: int = 3) -> bytes:
     return dst[:n].tobytes()
 
 
+def _raw_extract(data):
+    """content of a raw-block frame (parallel copy), or None for any other frame"""
+    from . import _native as nat
+    try:
+        L = nat.lib()
+    except Exception:
+        return None
+    n = ctypes.c_int64()
+    if L.xhe_zstd_raw_extract(data, len(data), None, 0, ctypes.byref(n)) != nat.XHE_EOVERFLOW or n.value < 2:
+        return None
+    out = bytes(n.value)
+    ptr = ctypes.cast(out, ctypes.c_void_p)
+    nat.advise_huge(ptr.value, n.value)
+    nat.check(L.xhe_zstd_raw_extract(data, len(data), ptr, n.value, ctypes.byref(n)), "zstd extract")
+    return out
+
+
 def decompress(data: bytes) -> bytes:
+    if len(data) >= RAW_FRAME_MIN:
+        out = _raw_extract(data)
+        if out is not None:
+            return out
     L = _lib()
     size = L.ZSTD_getFrameContentSize(data, len(data))
     if size >= (1 << 63):  # unknown / error

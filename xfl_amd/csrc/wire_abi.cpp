@@ -2,11 +2,13 @@
 // points and the error channel. Compiled by the host compiler and linked into
 // libxhe.so next to xhe.hip's object, so codec changes rebuild in seconds.
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <exception>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "../../include/xhe.h"
 #include "abi_common.hpp"
@@ -26,6 +28,9 @@ int guarded(F&& f) {
 
 // host threads for the codec: the machine's cores, at most 16 (a GPU box's
 // CPU share per GPU)
+constexpr int kZstdWindowLog = 17;
+constexpr int64_t kZstdBlock = (int64_t)1 << kZstdWindowLog;  // = the format's 128 KiB block maximum
+
 int codec_threads() {
   unsigned hc = std::thread::hardware_concurrency();
   return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
@@ -35,6 +40,16 @@ int codec_threads() {
 int xhe_fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+void xhe_host_copy(void* dst, const void* src, int64_t n) {
+  if (n <= 0) return;
+  const int T = n >= (8 << 20) ? codec_threads() : 1;
+  const int64_t per = ((n + T - 1) / T + 4095) & ~(int64_t)4095;
+  xhe::wire::run_parallel(T, [&](int t) {
+    const int64_t lo = (int64_t)t * per, hi = std::min<int64_t>(n, lo + per);
+    if (hi > lo) memcpy(static_cast<uint8_t*>(dst) + lo, static_cast<const uint8_t*>(src) + lo, hi - lo);
+  });
 }
 
 extern "C" {
@@ -50,6 +65,89 @@ int xhe_host_prefault(void* p, int64_t nbytes) {
   xhe::wire::run_parallel(T, [&](int t) {
     const int64_t lo = (int64_t)t * per, hi = std::min<int64_t>(nbytes, lo + per);
     for (int64_t o = lo; o < hi; o += 4096) base[o] = 0;
+  });
+  return XHE_OK;
+}
+
+int64_t xhe_zstd_raw_frame_size(int64_t n) {
+  const int64_t nb = n > 0 ? (n + kZstdBlock - 1) / kZstdBlock : 1;
+  return 14 + n + 3 * nb;
+}
+
+int xhe_zstd_raw_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len) {
+  // One zstd frame (RFC 8878) holding `src` as raw blocks: magic, a frame
+  // header with an 8-byte content size and a 128 KiB window (not single-
+  // segment, so streaming decoders need no content-sized window), then
+  // ceil(n / 128 KiB) raw blocks, the last one flagged. The layout is known
+  // in closed form, so the blocks are written by all codec threads at once.
+  if (!out_len || n < 0 || (n > 0 && !src)) return xhe_fail(XHE_EINVAL, "xhe_zstd_raw_frame: bad argument");
+  const int64_t need = xhe_zstd_raw_frame_size(n);
+  *out_len = need;
+  if (!dst || cap < need) return xhe_fail(XHE_EOVERFLOW, "xhe_zstd_raw_frame: output buffer too small");
+  static const uint8_t head[6] = {0x28, 0xB5, 0x2F, 0xFD, 0xC0, (uint8_t)((kZstdWindowLog - 10) << 3)};
+  memcpy(dst, head, 6);
+  for (int k = 0; k < 8; ++k) dst[6 + k] = (uint8_t)((uint64_t)n >> (8 * k));
+  const int64_t nb = n > 0 ? (n + kZstdBlock - 1) / kZstdBlock : 1;
+  const int T = n >= (8 << 20) ? codec_threads() : 1;
+  xhe::wire::run_parallel(T, [&](int t) {
+    for (int64_t b = nb * t / T; b < nb * (t + 1) / T; ++b) {
+      const int64_t lo = b * kZstdBlock, len = std::min<int64_t>(kZstdBlock, n - lo);
+      uint8_t* o = dst + 14 + b * (kZstdBlock + 3);
+      const uint32_t h = (uint32_t)(b == nb - 1) | (0u << 1) | ((uint32_t)len << 3);  // Last_Block, Raw, Block_Size
+      o[0] = (uint8_t)h;
+      o[1] = (uint8_t)(h >> 8);
+      o[2] = (uint8_t)(h >> 16);
+      if (len > 0) memcpy(o + 3, src + lo, len);
+    }
+  });
+  return XHE_OK;
+}
+
+int xhe_zstd_raw_extract(const uint8_t* src, int64_t len, uint8_t* dst, int64_t cap, int64_t* out_len) {
+  // The inverse for frames made only of raw blocks (what xhe_zstd_raw_frame
+  // writes): walk the block headers, then copy the payloads in parallel.
+  // Anything else - compressed or RLE blocks, a content checksum, a
+  // dictionary, trailing data, a missing content size - is XHE_ENOTSUP and
+  // left to libzstd.
+  if (!out_len || len < 0 || (len > 0 && !src)) return xhe_fail(XHE_EINVAL, "xhe_zstd_raw_extract: bad argument");
+  *out_len = -1;
+  auto unsup = [] { return xhe_fail(XHE_ENOTSUP, "not a raw-block zstd frame"); };
+  if (len < 6 || src[0] != 0x28 || src[1] != 0xB5 || src[2] != 0x2F || src[3] != 0xFD) return unsup();
+  const uint8_t fhd = src[4];
+  const int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1;
+  if ((fhd & 0x0F) != 0) return unsup();  // reserved bit, checksum or dictionary id
+  const int fcs_bytes = fcs_flag == 0 ? (single ? 1 : 0) : (1 << fcs_flag);
+  if (fcs_bytes == 0) return unsup();
+  int64_t pos = 5 + (single ? 0 : 1);
+  if (pos + fcs_bytes > len) return unsup();
+  uint64_t fcs = 0;
+  for (int k = 0; k < fcs_bytes; ++k) fcs |= (uint64_t)src[pos + k] << (8 * k);
+  if (fcs_bytes == 2) fcs += 256;
+  pos += fcs_bytes;
+  if (fcs > (uint64_t)INT64_MAX) return unsup();
+  std::vector<int64_t> from, to, size;
+  int64_t outp = 0;
+  for (bool last = false; !last;) {
+    if (pos + 3 > len) return unsup();
+    const uint32_t h = src[pos] | ((uint32_t)src[pos + 1] << 8) | ((uint32_t)src[pos + 2] << 16);
+    last = h & 1;
+    const int64_t bs = h >> 3;
+    pos += 3;
+    if (((h >> 1) & 3) != 0 || bs > len - pos || bs > (int64_t)fcs - outp) return unsup();
+    from.push_back(pos);
+    to.push_back(outp);
+    size.push_back(bs);
+    pos += bs;
+    outp += bs;
+  }
+  if (pos != len || outp != (int64_t)fcs) return unsup();
+  *out_len = outp;
+  if (!dst || cap < outp) return xhe_fail(XHE_EOVERFLOW, "xhe_zstd_raw_extract: output buffer too small");
+  const int64_t nb = (int64_t)from.size();
+  const int T = outp >= (8 << 20) ? codec_threads() : 1;
+  xhe::wire::run_parallel(T, [&](int t) {
+    for (int64_t b = nb * t / T; b < nb * (t + 1) / T; ++b)
+      if (size[b]) memcpy(dst + to[b], src + from[b], size[b]);
   });
   return XHE_OK;
 }
