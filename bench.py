@@ -260,7 +260,15 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
         ser.pop(0, None)
         ser[0] = Paillier.serialize(enc[0], compression=False)
     out["dropin_serialize_per_s"] = nh / _timed(ser_only, reps=3)
-    del enc, ser
+    # config 3's pairwise sum through the API: PaillierArray + PaillierArray
+    # (paillier.py:88-123 per element; host buffers in and out)
+    tot = {}
+
+    def add_only():
+        tot.pop(0, None)
+        tot[0] = enc[0] + enc[0]
+    out["dropin_add_per_s"] = nh / _timed(add_only, reps=3)
+    del enc, ser, tot
     t = _timed(lambda: Paillier.decrypt(ctx, Paillier.ciphertext_from(None, wire[False], compression=False)), reps=2)
     out["dropin_deserialize_decrypt_per_s"] = nh / t
     t = _timed(lambda: Paillier.ciphertext_from(None, wire[False], compression=False), reps=3)

@@ -5,8 +5,10 @@ The shared library is built in-tree (xfl_amd/lib/libxhe.so) by
 fallback: if the library or a GPU is missing, every entry point raises.
 """
 import ctypes
+import mmap
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -63,6 +65,10 @@ SIGNATURES = {
     "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64), _vp, ctypes.POINTER(ctypes.c_int)]),
     "xhe_host_prefault": (ctypes.c_int, [_vp, ctypes.c_int64]),
+    "xhe_zstd_raw_frame_size": (ctypes.c_int64, [ctypes.c_int64]),
+    "xhe_zstd_raw_frame": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "xhe_zstd_raw_extract": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int64)]),
     "xhe_profile": (ctypes.c_int, [ctypes.c_int]),
     "xhe_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64)]),
@@ -154,13 +160,65 @@ def advise_huge(addr, nbytes):
         pass
 
 
+class _HostBlock:
+    """Owner (the numpy base) of a recycled host allocation."""
+    __slots__ = ("__array_interface__", "mem", "__weakref__")
+
+
+_pool_lock = threading.Lock()
+_pool_free = {}       # nbytes -> [mmap]
+_pool_bytes = 0
+POOL_MAX_BYTES = 8 << 30   # freed result buffers kept for reuse, at most
+POOL_PER_SIZE = 4
+
+
+def _pool_release(mem, nbytes):
+    global _pool_bytes
+    with _pool_lock:
+        lst = _pool_free.setdefault(nbytes, [])
+        if _pool_bytes + nbytes <= POOL_MAX_BYTES and len(lst) < POOL_PER_SIZE:
+            lst.append(mem)
+            _pool_bytes += nbytes
+            return
+    # dropped: unmapped when the last reference goes
+
+
+def _pool_take(nbytes):
+    global _pool_bytes
+    with _pool_lock:
+        lst = _pool_free.get(nbytes)
+        if lst:
+            _pool_bytes -= nbytes
+            return lst.pop()
+    return None
+
+
 def empty(shape, dtype):
-    """np.empty for large host buffers the library writes into: hugepage-backed
-    and pre-faulted by the library's host threads (xhe_host_prefault)."""
-    a = np.empty(shape, dtype=dtype)
-    if a.nbytes >= (32 << 20):
-        advise_huge(a.ctypes.data, a.nbytes)
-        lib().xhe_host_prefault(ctypes.c_void_p(a.ctypes.data), ctypes.c_int64(a.nbytes))
+    """np.empty for the large host buffers the library writes results into
+    (ciphertext arrays of hundreds of MB). They come from a small cache of
+    anonymous mappings: when every array on a buffer has been released its
+    pages go back to the cache (up to POOL_MAX_BYTES), so a training loop's
+    next result of the same size lands in pages that are already faulted in
+    instead of paying the kernel's first-touch zero-fill again. Fresh mappings
+    are hugepage-advised and pre-faulted by the library's host threads."""
+    dt = np.dtype(dtype)
+    shape = tuple(int(d) for d in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    if nbytes < (32 << 20):
+        return np.empty(shape, dtype=dt)
+    mem = _pool_take(nbytes)
+    fresh = mem is None
+    if fresh:
+        mem = mmap.mmap(-1, nbytes)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(mem))
+    if fresh:
+        advise_huge(addr, nbytes)
+        lib().xhe_host_prefault(ctypes.c_void_p(addr), ctypes.c_int64(nbytes))
+    owner = _HostBlock()
+    owner.mem = mem
+    owner.__array_interface__ = {"data": (addr, False), "shape": shape, "typestr": dt.str, "version": 3}
+    a = np.asarray(owner)
+    weakref.finalize(owner, _pool_release, mem, nbytes)
     return a
 
 
