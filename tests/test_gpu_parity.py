@@ -60,7 +60,8 @@ def test_decrypt_bit_exact(fx, case):
 
 
 def test_host_encrypt_chunking_is_invisible():
-    """xhe_encrypt_f64_host pipelines 64k-element chunks over two streams; the
+    """xhe_encrypt_f64_host pipelines 128k-element chunks (compute stream +
+    copy streams, pinned staging); the
     randomness is drawn at global element positions, so the result equals one
     device-resident encode + draw + encrypt of the whole batch, and spot
     elements equal the oracle's encryption with the drawn a."""

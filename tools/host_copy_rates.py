@@ -53,7 +53,7 @@ def main():
             fn()
         return (time.time() - t0) / args.reps
 
-    out = {"n": N, "win": args.win}
+    out = {"n": N, "win": args.win, "host_chunk": os.environ.get("XHE_HOST_CHUNK", "default")}
     out["fresh_np_empty_per_s"] = N / timed(lambda: host_enc(np.empty((N, dk.n2w), np.uint32)))
     out["fresh_nat_empty_per_s"] = N / timed(lambda: host_enc(nat.empty((N, dk.n2w), np.uint32)))
     keep = np.empty((N, dk.n2w), np.uint32)
@@ -71,6 +71,14 @@ def main():
     nat.check(L.xhe_rand(dk.handle, seed, 9, N, r.data_ptr(), None, stream), "rand")
     nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), r.data_ptr(), N, c.data_ptr(), stream), "encrypt")
     torch.cuda.synchronize()
+
+    def device_step():
+        nat.check(L.xhe_encode_f64(dk.handle, xd.data_ptr(), N, 7, 0, 0, m.data_ptr(), e.data_ptr(), s_.data_ptr(),
+                                   stream), "encode")
+        nat.check(L.xhe_rand(dk.handle, seed, 9, N, r.data_ptr(), None, stream), "rand")
+        nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), r.data_ptr(), N, c.data_ptr(), stream), "encrypt")
+        torch.cuda.synchronize()
+    out["device_resident_per_s"] = N / timed(device_step)
     out["host_equals_device"] = bool(np.array_equal(c.cpu().numpy().view(np.uint32), keep)
                                      and np.array_equal(e.cpu().numpy(), ex))
     ctx = PaillierContext().init(p, q, djn_h_pow_n=h)

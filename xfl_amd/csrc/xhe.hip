@@ -4,7 +4,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -500,6 +502,55 @@ int blocks_for(int64_t count, int tpi, int cap) {
   return (int)std::min<int64_t>(b, cap);
 }
 
+// Workspaces of the kernel entry points. Normally stream-ordered pool
+// allocations; inside a host pipeline's chunk (t_ws set) they come from that
+// chunk slot's cache and are kept for the whole call: with the pool, a
+// workspace freed on one slot's stream and wanted by the next slot's call
+// made hipMallocAsync hold the host until the first stream drained, which
+// serialised the pipeline. Reuse within a slot is safe: its calls run in
+// stream order, and a slot is reused only after its stream has drained.
+struct WsCache {
+  struct Blk {
+    void* p;
+    size_t bytes;
+    bool used;
+  };
+  std::vector<Blk> blk;
+  hipStream_t s = nullptr;
+  WsCache() = default;
+  WsCache(const WsCache&) = delete;
+  WsCache& operator=(const WsCache&) = delete;
+  ~WsCache() {
+    for (auto& b : blk) (void)hipFreeAsync(b.p, s);
+  }
+};
+thread_local WsCache* t_ws = nullptr;
+
+void ws_alloc(void** p, size_t bytes, hipStream_t s) {
+  if (t_ws) {
+    for (auto& b : t_ws->blk)
+      if (!b.used && b.bytes >= bytes) {
+        b.used = true;
+        *p = b.p;
+        return;
+      }
+    HIPCHK(hipMallocAsync(p, bytes, s));
+    t_ws->blk.push_back({*p, bytes, true});
+    return;
+  }
+  HIPCHK(hipMallocAsync(p, bytes, s));
+}
+
+void ws_free(void* p, hipStream_t s) {
+  if (t_ws)
+    for (auto& b : t_ws->blk)
+      if (b.p == p) {
+        b.used = false;
+        return;
+      }
+  HIPCHK(hipFreeAsync(p, s));
+}
+
 constexpr int64_t kChunk = 1 << 20;  // elements per launch chunk (bounds workspace)
 
 // ---- optional per-kernel timing (hipEvents on the launch stream)
@@ -566,7 +617,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   using MP2 = typename Sh::MP2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
@@ -597,7 +648,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     }
     crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 // grid for per-group-workspace (grid-stride) kernels
@@ -612,7 +663,7 @@ void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r
   using MN2 = typename Sh::MN2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)MN2::S4 * chunk * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)MN2::S4 * chunk * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MN2::TPI + 255) / 256);
@@ -621,7 +672,7 @@ void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r
                        r + (size_t)off * k->rand_words, k->rand_words, n, ws, ct + (size_t)off * k->n2w);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 template <class Sh>
@@ -637,8 +688,8 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
     int pb = pow_grid<MPE>(chunk, 512);
     int64_t groups = (int64_t)pb * 256 / MPE::TPI;
     uint32_t *ws = nullptr, *rows = nullptr;
-    HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 18 * MPE::S4 * groups * sizeof(uint32_t), s));
-    HIPCHK(hipMallocAsync((void**)&rows, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+    ws_alloc((void**)&ws, (size_t)2 * 18 * MPE::S4 * groups * sizeof(uint32_t), s);
+    ws_alloc((void**)&rows, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s);
     for (int64_t off = 0; off < count; off += chunk) {
       int64_t n = std::min(chunk, count - off);
       {
@@ -651,15 +702,15 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
       }
       crt_enc_launch<Sh>(k, n, rows, ct + (size_t)off * k->n2w, s);
     }
-    HIPCHK(hipFreeAsync(ws, s));
-    HIPCHK(hipFreeAsync(rows, s));
+    ws_free(ws, s);
+    ws_free(rows, s);
   } else {
     using MN2 = typename Sh::MN2;
     int64_t chunk = std::min<int64_t>(count, kChunk);
     int pb = pow_grid<MN2>(chunk, 512);
     int64_t groups = (int64_t)pb * 256 / MN2::TPI;
     uint32_t* ws = nullptr;
-    HIPCHK(hipMallocAsync((void**)&ws, (size_t)18 * MN2::S4 * groups * sizeof(uint32_t), s));
+    ws_alloc((void**)&ws, (size_t)18 * MN2::S4 * groups * sizeof(uint32_t), s);
     for (int64_t off = 0; off < count; off += chunk) {
       int64_t n = std::min(chunk, count - off);
       ProfScope ps("k_nodjn_pub", s);
@@ -667,7 +718,7 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
                          r + (size_t)off * k->rand_words, k->rand_words, n, ct + (size_t)off * k->n2w, ws);
       HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipFreeAsync(ws, s));
+    ws_free(ws, s);
   }
 }
 
@@ -697,7 +748,7 @@ void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const u
                  int64_t count, int dmax, uint32_t* out, int32_t* eout, hipStream_t s) {
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * MN2::S4 * chunk * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)2 * MN2::S4 * chunk * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MN2::TPI + 255) / 256);
@@ -706,7 +757,7 @@ void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const u
                        out + (size_t)off * k->n2w, eout ? eout + off : nullptr, ws);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 template <class Sh, class MN2 = typename Sh::MN2>
@@ -716,7 +767,7 @@ void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int k
   int pb = pow_grid<MN2>(chunk, 512);
   int64_t groups = (int64_t)pb * 256 / MN2::TPI;
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)17 * MN2::S4 * groups * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)17 * MN2::S4 * groups * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     ProfScope ps("k_powmod_n2", s);
@@ -724,7 +775,7 @@ void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int k
                        kw_ + (size_t)off * kw, kw, kbits, n, out + (size_t)off * k->n2w, ws);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 // Batch inversion mod n^2 via a product tree (Montgomery's trick in parallel).
@@ -919,7 +970,7 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
   using MP2 = typename Sh::MP2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
@@ -927,7 +978,7 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
                        ct + (size_t)off * k->n2w);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 // Decrypt exponentiation shapes by batch size (latency- vs throughput-bound):
@@ -954,7 +1005,7 @@ void dec_pow_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
   int pow_blocks = (int)std::min<int64_t>((chunk * MP2S::TPI + 255) / 256, 512);
   int64_t groups = (int64_t)pow_blocks * 256 / MP2S::TPI;
   uint32_t* ws = nullptr;
-  HIPCHK(hipMallocAsync((void**)&ws, (size_t)2 * 17 * MP2S::S4 * groups * sizeof(uint32_t), s));
+  ws_alloc((void**)&ws, (size_t)2 * 17 * MP2S::S4 * groups * sizeof(uint32_t), s);
   const ModDev& mp = SHAPE == 2 ? k->kd.p2X : SHAPE == 1 ? k->kd.p2L : k->kd.p2;
   const ModDev& mq = SHAPE == 2 ? k->kd.q2X : SHAPE == 1 ? k->kd.q2L : k->kd.q2;
   {
@@ -963,7 +1014,7 @@ void dec_pow_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
                        (int)MP2::S4, xrows, ws);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(ws, s));
+  ws_free(ws, s);
 }
 
 template <class Sh>
@@ -980,8 +1031,8 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
                                                                    : 1;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t *xrows = nullptr, *mrows = nullptr;
-  HIPCHK(hipMallocAsync((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s));
-  HIPCHK(hipMallocAsync((void**)&mrows, (size_t)2 * 2 * MP::S4 * chunk * sizeof(uint32_t), s));
+  ws_alloc((void**)&xrows, (size_t)2 * MP2::S4 * chunk * sizeof(uint32_t), s);
+  ws_alloc((void**)&mrows, (size_t)2 * 2 * MP::S4 * chunk * sizeof(uint32_t), s);
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     const uint32_t* cto = ct + (size_t)off * k->n2w;
@@ -996,8 +1047,8 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
                        m + (size_t)off * k->nw);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipFreeAsync(xrows, s));
-  HIPCHK(hipFreeAsync(mrows, s));
+  ws_free(xrows, s);
+  ws_free(mrows, s);
 }
 
 template <class F>
@@ -1049,6 +1100,219 @@ struct Stream {
     (void)hipStreamDestroy(s);
   }
 };
+
+// The stream-ordered allocator (hipMallocAsync, every call's workspaces)
+// returns freed memory to the device at each synchronisation by default
+// (release threshold 0), so a host-buffer call that syncs per chunk would map
+// fresh pages for every chunk's workspace. Keep up to kPoolKeep bytes cached
+// in the device's default pool instead (set once per device, at key creation).
+constexpr uint64_t kPoolKeep = 16ull << 30;
+void keep_pool_memory(int device) {
+  static std::mutex mu;
+  static bool done[64] = {};
+  std::lock_guard<std::mutex> g(mu);
+  if (device < 0 || device >= 64 || done[device]) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t keep = kPoolKeep;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  done[device] = true;
+}
+
+// Pinned staging ring for the host-buffer entry points. A copy between the
+// device and pageable memory goes through the runtime's small bounce buffers
+// (~10 GB/s) and holds the calling thread; from or into pinned memory it is
+// one DMA at the link rate and asynchronous. One ring per device is kept for
+// the process lifetime and grown on demand; a call that finds it in use by
+// another thread gets a ring of its own. Slot b holds one chunk's parts
+// (inputs and outputs) at fixed offsets.
+class PinnedSlots {
+ public:
+  PinnedSlots(int device, int depth, const std::vector<size_t>& part_bytes) {
+    size_t off = 0;
+    for (size_t b : part_bytes) {
+      off_.push_back(off);
+      off += (b + 255) & ~(size_t)255;
+    }
+    slot_ = off;
+    const size_t need = std::max<size_t>(slot_ * depth, 256);
+    Ring& r = ring(device);
+    lock_ = std::unique_lock<std::mutex>(r.mu, std::try_to_lock);
+    if (lock_.owns_lock()) {
+      if (r.bytes < need) {
+        if (r.p) HIPCHK(hipHostFree(r.p));
+        r.p = nullptr;
+        r.bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&r.p, need, hipHostMallocDefault));
+        r.bytes = need;
+      }
+      base_ = r.p;
+    } else {
+      HIPCHK(hipHostMalloc((void**)&own_, need, hipHostMallocDefault));
+      base_ = own_;
+    }
+  }
+  ~PinnedSlots() {
+    if (own_) (void)hipHostFree(own_);
+  }
+  PinnedSlots(const PinnedSlots&) = delete;
+  PinnedSlots& operator=(const PinnedSlots&) = delete;
+  uint8_t* at(int b, int k) const { return base_ + (size_t)b * slot_ + off_[k]; }
+
+ private:
+  struct Ring {
+    std::mutex mu;
+    uint8_t* p = nullptr;
+    size_t bytes = 0;
+  };
+  static Ring& ring(int device) {
+    static Ring rings[64];
+    return rings[device & 63];
+  }
+  std::vector<size_t> off_;
+  size_t slot_ = 0;
+  std::unique_lock<std::mutex> lock_;
+  uint8_t* base_ = nullptr;
+  uint8_t* own_ = nullptr;
+};
+
+// A per-element host buffer of an element-chunked host call: elem_bytes per
+// element; host == nullptr marks an absent optional argument.
+struct HostPart {
+  const void* host;
+  size_t elem_bytes;
+};
+
+// Elements per chunk of the host-buffer pipelines for the encryption kernels
+// ($XHE_HOST_CHUNK overrides, for A/B runs).
+int64_t host_chunk(int64_t dflt) {
+  static const int64_t v = [] {
+    const char* e = getenv("XHE_HOST_CHUNK");
+    return e ? std::max<int64_t>(1024, atoll(e)) : (int64_t)0;
+  }();
+  return v ? v : dflt;
+}
+
+// RAII hipEvent without timing (ordering only)
+struct Event {
+  hipEvent_t e = nullptr;
+  Event() { HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
+  ~Event() { (void)hipEventDestroy(e); }
+};
+
+// Element-chunked host-buffer call. Chunk c uses slot b = c % depth and
+// stream b: host threads copy its inputs into pinned slot b (xhe_host_copy),
+// the upload, run(b, off, n, din, dout, stream)'s kernels and the download
+// into the slot follow in stream order, and once the download has landed host
+// threads copy the results into the caller's buffers. Chunk c + depth - 1 is
+// staged and enqueued before chunk c is drained, so the host copies and both
+// DMA directions overlap the kernels. The kernels of chunk c wait for those of
+// chunk c - 1 (an event): kernels of different chunks never share the CUs (a
+// big kernel next to a small one on another stream stretches the small one
+// from microseconds to milliseconds and stalls the chain behind it), while
+// each copy stays in its own stream behind its own kernels, where the runtime
+// gives it to a DMA engine (a cross-stream wait in front of a copy made the
+// runtime run it as a blit kernel on the CUs instead). Batches whose chunk
+// moves < 1 MiB copy straight from and to the caller's memory.
+template <class Run>
+int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::vector<HostPart>& in,
+                  const std::vector<HostPart>& out, Run&& run) {
+  if (count <= 0) return XHE_OK;
+  static const bool trace = getenv("XHE_HOST_TRACE") != nullptr;  // per-chunk timings to stderr
+  static const bool serial = getenv("XHE_HOST_SERIAL") != nullptr;  // chunk kernels one after another (A/B)
+  chunk = std::max<int64_t>(1, std::min(chunk, count));
+  const int64_t nch = (count + chunk - 1) / chunk;
+  const int D = (int)std::min<int64_t>(nch, 3);
+  const int ni = (int)in.size(), no = (int)out.size();
+  std::vector<size_t> parts;
+  size_t per_chunk = 0;
+  for (auto& h : in) parts.push_back(h.elem_bytes * chunk), per_chunk += h.elem_bytes * chunk;
+  for (auto& h : out) parts.push_back(h.elem_bytes * chunk), per_chunk += h.elem_bytes * chunk;
+  const bool staged = per_chunk >= ((size_t)1 << 20);
+  Stream st[3];
+  Event ev_k[3];
+  WsCache wsc[3];  // destroyed before the streams (frees are stream-ordered)
+  for (int b = 0; b < 3; ++b) wsc[b].s = st[b].s;
+  std::vector<std::unique_ptr<DevBuf>> dev;  // [slot][part]
+  for (int b = 0; b < D; ++b)
+    for (size_t k = 0; k < parts.size(); ++k) dev.emplace_back(new DevBuf(parts[k], st[b].s));
+  std::unique_ptr<PinnedSlots> pin;
+  if (staged) pin.reset(new PinnedSlots(key->device, D, parts));
+  auto dptr = [&](int b, int k) { return dev[(size_t)b * parts.size() + k]->p; };
+  auto enqueue = [&](int64_t c) -> int {
+    const int b = (int)(c % D);
+    const int64_t off = c * chunk, n = std::min(chunk, count - off);
+    hipStream_t s = st[b].s;
+    const auto tin = std::chrono::steady_clock::now();
+    std::vector<void*> din(ni), dout(no);
+    for (int k = 0; k < ni; ++k) {
+      din[k] = in[k].host ? dptr(b, k) : nullptr;
+      if (!in[k].host) continue;
+      const uint8_t* src = static_cast<const uint8_t*>(in[k].host) + (size_t)off * in[k].elem_bytes;
+      const size_t nb = (size_t)n * in[k].elem_bytes;
+      if (staged) {
+        xhe_host_copy(pin->at(b, k), src, (int64_t)nb);
+        src = pin->at(b, k);
+      }
+      HIPCHK(hipMemcpyAsync(din[k], src, nb, hipMemcpyHostToDevice, s));
+    }
+    if (trace)
+      fprintf(stderr, "[host_pipeline] chunk %lld: staged inputs %.3f ms\n", (long long)c,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tin).count());
+    if (serial && c > 0) HIPCHK(hipStreamWaitEvent(s, ev_k[(c - 1) % D].e, 0));
+    for (int k = 0; k < no; ++k) dout[k] = out[k].host ? dptr(b, ni + k) : nullptr;
+    const auto tr = std::chrono::steady_clock::now();
+    for (auto& w : wsc[b].blk) w.used = false;
+    t_ws = &wsc[b];
+    int rc;
+    try {
+      rc = run(b, off, n, din.data(), dout.data(), s);
+    } catch (...) {
+      t_ws = nullptr;
+      throw;
+    }
+    t_ws = nullptr;
+    if (rc != XHE_OK) return rc;
+    HIPCHK(hipEventRecord(ev_k[b].e, s));
+    const auto td = std::chrono::steady_clock::now();
+    for (int k = 0; k < no; ++k)
+      if (out[k].host) {
+        void* dst = staged ? (void*)pin->at(b, ni + k)
+                           : (void*)(static_cast<uint8_t*>(const_cast<void*>(out[k].host)) + (size_t)off * out[k].elem_bytes);
+        HIPCHK(hipMemcpyAsync(dst, dout[k], (size_t)n * out[k].elem_bytes, hipMemcpyDeviceToHost, s));
+      }
+    if (trace)
+      fprintf(stderr, "[host_pipeline] chunk %lld: run %.3f ms, d2h enqueue %.3f ms\n", (long long)c,
+              std::chrono::duration<double, std::milli>(td - tr).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count());
+    return XHE_OK;
+  };
+  int rc = XHE_OK;
+  for (int64_t c = 0; c + 1 < D; ++c)
+    if ((rc = enqueue(c)) != XHE_OK) return rc;
+  for (int64_t c = 0; c < nch; ++c) {
+    // slot (c - 1) % D was drained last iteration (its stream has finished)
+    if (c + D - 1 < nch && (rc = enqueue(c + D - 1)) != XHE_OK) return rc;
+    const int b = (int)(c % D);
+    const int64_t off = c * chunk, n = std::min(chunk, count - off);
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipStreamSynchronize(st[b].s));
+    const auto t1 = std::chrono::steady_clock::now();
+    if (staged)
+      for (int k = 0; k < no; ++k)
+        if (out[k].host)
+          xhe_host_copy(static_cast<uint8_t*>(const_cast<void*>(out[k].host)) + (size_t)off * out[k].elem_bytes,
+                        pin->at(b, ni + k), (int64_t)((size_t)n * out[k].elem_bytes));
+    if (trace) {
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr, "[host_pipeline] chunk %lld: wait %.3f ms, copy-out %.3f ms\n", (long long)c,
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
+  }
+  return XHE_OK;
+}
 }  // namespace
 
 namespace {
@@ -1125,6 +1389,7 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     }
     if (k->djn) h = BigU::from_words(h_pow_n_words, k->n2w);
     DevGuard dg(device);
+    keep_pool_memory(device);
     key_create_impl(k.get(), n, k->priv ? &p : nullptr, k->priv ? &q : nullptr, k->djn ? &h : nullptr, win_bits);
     *out = k.release();
     return XHE_OK;
@@ -1229,36 +1494,17 @@ int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev
   });
 }
 
-static int host_roundtrip(const xhe_key* key, const uint32_t* in, size_t in_words, uint32_t* outp, size_t out_words,
-                          const uint32_t* in2, size_t in2_words, bool enc) {
-  DevGuard dg(key->device);
-  hipStream_t s;
-  HIPCHK(hipStreamCreate(&s));
-  uint32_t *d_in = nullptr, *d_in2 = nullptr, *d_out = nullptr;
-  HIPCHK(hipMalloc(&d_in, std::max<size_t>(in_words, 1) * 4));
-  HIPCHK(hipMalloc(&d_out, std::max<size_t>(out_words, 1) * 4));
-  if (in2) HIPCHK(hipMalloc(&d_in2, std::max<size_t>(in2_words, 1) * 4));
-  HIPCHK(hipMemcpyAsync(d_in, in, in_words * 4, hipMemcpyHostToDevice, s));
-  if (in2) HIPCHK(hipMemcpyAsync(d_in2, in2, in2_words * 4, hipMemcpyHostToDevice, s));
-  int rc;
-  int64_t count = enc ? (int64_t)(in_words / key->nw) : (int64_t)(in_words / key->n2w);
-  if (enc) rc = xhe_encrypt(key, d_in, d_in2, count, d_out, s);
-  else rc = xhe_decrypt(key, d_in, count, d_out, s);
-  if (rc == XHE_OK) HIPCHK(hipMemcpyAsync(outp, d_out, out_words * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  (void)hipFree(d_in);
-  (void)hipFree(d_out);
-  if (d_in2) (void)hipFree(d_in2);
-  (void)hipStreamDestroy(s);
-  return rc;
-}
-
 int xhe_encrypt_host(const xhe_key* key, const uint32_t* m, const uint32_t* rand, int64_t count, uint32_t* ct) {
   return guarded([&]() -> int {
     if (!key || (count > 0 && (!m || !ct))) return fail(XHE_EINVAL, "xhe_encrypt_host: null argument");
     if (count <= 0) return XHE_OK;
-    return host_roundtrip(key, m, (size_t)count * key->nw, ct, (size_t)count * key->n2w, rand,
-                          rand ? (size_t)count * key->rand_words : 0, true);
+    DevGuard dg(key->device);
+    return host_pipeline(key, count, 1 << 17, {{m, (size_t)key->nw * 4}, {rand, (size_t)key->rand_words * 4}},
+                         {{ct, (size_t)key->n2w * 4}},
+                         [&](int, int64_t, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+                           return xhe_encrypt(key, (const uint32_t*)din[0], (const uint32_t*)din[1], n,
+                                              (uint32_t*)dout[0], s);
+                         });
   });
 }
 
@@ -1267,7 +1513,11 @@ int xhe_decrypt_host(const xhe_key* key, const uint32_t* ct, int64_t count, uint
     if (!key || (count > 0 && (!ct || !m))) return fail(XHE_EINVAL, "xhe_decrypt_host: null argument");
     if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
     if (count <= 0) return XHE_OK;
-    return host_roundtrip(key, ct, (size_t)count * key->n2w, m, (size_t)count * key->nw, nullptr, 0, false);
+    DevGuard dg(key->device);
+    return host_pipeline(key, count, 1 << 17, {{ct, (size_t)key->n2w * 4}}, {{m, (size_t)key->nw * 4}},
+                         [&](int, int64_t, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+                           return xhe_decrypt(key, (const uint32_t*)din[0], n, (uint32_t*)dout[0], s);
+                         });
   });
 }
 
@@ -1331,48 +1581,25 @@ int xhe_encrypt_f64_host(const xhe_key* key, const double* x, int64_t count, int
       return fail(XHE_EINVAL, "xhe_encrypt_f64_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    // Chunks alternate between two streams: chunk i+1's upload and kernels are
-    // enqueued before chunk i's (host-blocking, pageable) download, so the
-    // PCIe copy-out of one chunk overlaps the kernels of the next. The
-    // randomness is drawn at global element positions, so the ciphertexts do
-    // not depend on the chunking.
-    const int64_t chunk = count >= (1 << 17) ? (1 << 16) : count;
-    const int64_t nch = (count + chunk - 1) / chunk;
-    Stream st[2];
-    std::unique_ptr<DevBuf> dx[2], dm[2], de[2], ds[2], dc[2], dr[2];
-    for (int b = 0; b < (nch > 1 ? 2 : 1); ++b) {
-      dx[b].reset(new DevBuf(chunk * 8, st[b].s));
-      dm[b].reset(new DevBuf((size_t)chunk * key->nw * 4, st[b].s));
-      de[b].reset(new DevBuf(chunk * 4, st[b].s));
-      ds[b].reset(new DevBuf(chunk * 4, st[b].s));
-      dc[b].reset(new DevBuf((size_t)chunk * key->n2w * 4, st[b].s));
-      dr[b].reset(new DevBuf(obfuscate ? (size_t)chunk * key->rand_words * 4 : 4, st[b].s));
-    }
-    auto enqueue = [&](int64_t c) -> int {
-      const int b = (int)(c & 1);
-      const int64_t off = c * chunk, n = std::min(chunk, count - off);
-      hipStream_t s = st[b].s;
-      HIPCHK(hipMemcpyAsync(dx[b]->p, x + off, n * 8, hipMemcpyHostToDevice, s));
-      int rc = xhe_encode_f64(key, dx[b]->as<double>(), n, precision, has_max, max_exponent, dm[b]->as<uint32_t>(),
-                              de[b]->as<int32_t>(), ds[b]->as<int32_t>(), s);
-      if (rc != XHE_OK) return rc;
-      if (obfuscate) rand_impl(key, seed32, nonce, off, n, dr[b]->as<uint32_t>(), nullptr, s);
-      return xhe_encrypt(key, dm[b]->as<uint32_t>(), obfuscate ? dr[b]->as<uint32_t>() : nullptr, n,
-                         dc[b]->as<uint32_t>(), s);
-    };
-    int rc = enqueue(0);
-    if (rc != XHE_OK) return rc;
-    for (int64_t c = 0; c < nch; ++c) {
-      if (c + 1 < nch && (rc = enqueue(c + 1)) != XHE_OK) return rc;
-      const int b = (int)(c & 1);
-      const int64_t off = c * chunk, n = std::min(chunk, count - off);
-      hipStream_t s = st[b].s;
-      HIPCHK(hipMemcpyAsync(ct + (size_t)off * key->n2w, dc[b]->p, (size_t)n * key->n2w * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(exps + off, de[b]->p, n * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(status + off, ds[b]->p, n * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));  // chunk c+2 reuses buffer b
-    }
-    return XHE_OK;
+    // chunks of 128 k elements (2,048 waves: one full round of the chip) through
+    // host_pipeline; the randomness is drawn at global element positions, so
+    // the ciphertexts do not depend on the chunking
+    const int64_t chunk = host_chunk(1 << 17), cmax = std::min<int64_t>(chunk, count);
+    std::unique_ptr<DevBuf> dm[3], dr[3];
+    return host_pipeline(
+        key, count, chunk, {{x, 8}}, {{ct, (size_t)key->n2w * 4}, {exps, 4}, {status, 4}},
+        [&](int b, int64_t off, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+          if (!dm[b]) {
+            dm[b].reset(new DevBuf((size_t)cmax * key->nw * 4, s));
+            dr[b].reset(new DevBuf(obfuscate ? (size_t)cmax * key->rand_words * 4 : 4, s));
+          }
+          int rc = xhe_encode_f64(key, (const double*)din[0], n, precision, has_max, max_exponent,
+                                  dm[b]->as<uint32_t>(), (int32_t*)dout[1], (int32_t*)dout[2], s);
+          if (rc != XHE_OK) return rc;
+          if (obfuscate) rand_impl(key, seed32, nonce, off, n, dr[b]->as<uint32_t>(), nullptr, s);
+          return xhe_encrypt(key, dm[b]->as<uint32_t>(), obfuscate ? dr[b]->as<uint32_t>() : nullptr, n,
+                             (uint32_t*)dout[0], s);
+        });
   });
 }
 
@@ -1383,20 +1610,18 @@ int xhe_encrypt_words_host(const xhe_key* key, const uint32_t* m, int64_t count,
       return fail(XHE_EINVAL, "xhe_encrypt_words_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    Stream st;
-    DevBuf dm((size_t)count * key->nw * 4, st.s), dc((size_t)count * key->n2w * 4, st.s),
-        dr(obfuscate ? (size_t)count * key->rand_words * 4 : 4, st.s);
-    HIPCHK(hipMemcpyAsync(dm.p, m, (size_t)count * key->nw * 4, hipMemcpyHostToDevice, st.s));
-    int rc = XHE_OK;
-    if (obfuscate) {
-      rc = xhe_rand(key, seed32, nonce, count, dr.as<uint32_t>(), nullptr, st.s);
-      if (rc != XHE_OK) return rc;
-    }
-    rc = xhe_encrypt(key, dm.as<uint32_t>(), obfuscate ? dr.as<uint32_t>() : nullptr, count, dc.as<uint32_t>(), st.s);
-    if (rc != XHE_OK) return rc;
-    HIPCHK(hipMemcpyAsync(ct, dc.p, (size_t)count * key->n2w * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipStreamSynchronize(st.s));
-    return XHE_OK;
+    const int64_t chunk = host_chunk(1 << 17), cmax = std::min<int64_t>(chunk, count);
+    std::unique_ptr<DevBuf> dr[3];
+    return host_pipeline(
+        key, count, chunk, {{m, (size_t)key->nw * 4}}, {{ct, (size_t)key->n2w * 4}},
+        [&](int b, int64_t off, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+          if (obfuscate) {
+            if (!dr[b]) dr[b].reset(new DevBuf((size_t)cmax * key->rand_words * 4, s));
+            rand_impl(key, seed32, nonce, off, n, dr[b]->as<uint32_t>(), nullptr, s);
+          }
+          return xhe_encrypt(key, (const uint32_t*)din[0], obfuscate ? dr[b]->as<uint32_t>() : nullptr, n,
+                             (uint32_t*)dout[0], s);
+        });
   });
 }
 
@@ -1408,22 +1633,22 @@ int xhe_decrypt_decode_host(const xhe_key* key, const uint32_t* ct, const int32_
     if (!key->priv) return fail(XHE_EINVAL, "Try to decrypt a paillier ciphertext by a public key.");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    Stream st;
-    DevBuf dc((size_t)count * key->n2w * 4, st.s), dm((size_t)count * key->nw * 4, st.s), de(count * 4, st.s),
-        d64(count * 8, st.s), d32(count * 4, st.s), ds(count * 4, st.s);
-    HIPCHK(hipMemcpyAsync(dc.p, ct, (size_t)count * key->n2w * 4, hipMemcpyHostToDevice, st.s));
-    HIPCHK(hipMemcpyAsync(de.p, exps, count * 4, hipMemcpyHostToDevice, st.s));
-    int rc = xhe_decrypt(key, dc.as<uint32_t>(), count, dm.as<uint32_t>(), st.s);
-    if (rc != XHE_OK) return rc;
-    rc = xhe_decode(key, dm.as<uint32_t>(), de.as<int32_t>(), count, d64.as<double>(), d32.as<float>(),
-                    ds.as<int32_t>(), st.s);
-    if (rc != XHE_OK) return rc;
-    HIPCHK(hipMemcpyAsync(f64, d64.p, count * 8, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipMemcpyAsync(f32, d32.p, count * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipMemcpyAsync(status, ds.p, count * 4, hipMemcpyDeviceToHost, st.s));
-    if (m_out) HIPCHK(hipMemcpyAsync(m_out, dm.p, (size_t)count * key->nw * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipStreamSynchronize(st.s));
-    return XHE_OK;
+    const int64_t chunk = host_chunk(1 << 17), cmax = std::min<int64_t>(chunk, count);
+    std::unique_ptr<DevBuf> dm[3];
+    return host_pipeline(
+        key, count, chunk, {{ct, (size_t)key->n2w * 4}, {exps, 4}},
+        {{f64, 8}, {f32, 4}, {status, 4}, {m_out, (size_t)key->nw * 4}},
+        [&](int b, int64_t, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+          uint32_t* m = (uint32_t*)dout[3];
+          if (!m) {
+            if (!dm[b]) dm[b].reset(new DevBuf((size_t)cmax * key->nw * 4, s));
+            m = dm[b]->as<uint32_t>();
+          }
+          int rc = xhe_decrypt(key, (const uint32_t*)din[0], n, m, s);
+          if (rc != XHE_OK) return rc;
+          return xhe_decode(key, m, (const int32_t*)din[1], n, (double*)dout[0], (float*)dout[1],
+                            (int32_t*)dout[2], s);
+        });
   });
 }
 
@@ -1433,21 +1658,13 @@ int xhe_mulmod_host(const xhe_key* key, const uint32_t* a, const int32_t* ea, co
     if (!key || (count > 0 && (!a || !b || !out))) return fail(XHE_EINVAL, "xhe_mulmod_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    Stream st;
-    size_t cw = (size_t)count * key->n2w * 4;
-    DevBuf da(cw, st.s), db(cw, st.s), dout(cw, st.s), dea(count * 4, st.s), deb(count * 4, st.s), deo(count * 4, st.s);
-    HIPCHK(hipMemcpyAsync(da.p, a, cw, hipMemcpyHostToDevice, st.s));
-    HIPCHK(hipMemcpyAsync(db.p, b, cw, hipMemcpyHostToDevice, st.s));
-    if (ea) HIPCHK(hipMemcpyAsync(dea.p, ea, count * 4, hipMemcpyHostToDevice, st.s));
-    if (eb) HIPCHK(hipMemcpyAsync(deb.p, eb, count * 4, hipMemcpyHostToDevice, st.s));
-    int rc = xhe_mulmod(key, da.as<uint32_t>(), ea ? dea.as<int32_t>() : nullptr, db.as<uint32_t>(),
-                        eb ? deb.as<int32_t>() : nullptr, count, dmax, dout.as<uint32_t>(),
-                        eout ? deo.as<int32_t>() : nullptr, st.s);
-    if (rc != XHE_OK) return rc;
-    HIPCHK(hipMemcpyAsync(out, dout.p, cw, hipMemcpyDeviceToHost, st.s));
-    if (eout) HIPCHK(hipMemcpyAsync(eout, deo.p, count * 4, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipStreamSynchronize(st.s));
-    return XHE_OK;
+    const size_t cb = (size_t)key->n2w * 4;
+    return host_pipeline(
+        key, count, 1 << 16, {{a, cb}, {ea, 4}, {b, cb}, {eb, 4}}, {{out, cb}, {eout, 4}},
+        [&](int, int64_t, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+          return xhe_mulmod(key, (const uint32_t*)din[0], (const int32_t*)din[1], (const uint32_t*)din[2],
+                            (const int32_t*)din[3], n, dmax, (uint32_t*)dout[0], (int32_t*)dout[1], s);
+        });
   });
 }
 
@@ -1457,22 +1674,21 @@ int xhe_powmod_host(const xhe_key* key, const uint32_t* c, const uint32_t* k, in
     if (!key || (count > 0 && (!c || !k || !out))) return fail(XHE_EINVAL, "xhe_powmod_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    Stream st;
-    size_t cw = (size_t)count * key->n2w * 4;
-    DevBuf dc(cw, st.s), dk((size_t)count * kw * 4, st.s), dout(cw, st.s), dinv(invert_first ? cw : 4, st.s);
-    HIPCHK(hipMemcpyAsync(dc.p, c, cw, hipMemcpyHostToDevice, st.s));
-    HIPCHK(hipMemcpyAsync(dk.p, k, (size_t)count * kw * 4, hipMemcpyHostToDevice, st.s));
-    const uint32_t* base = dc.as<uint32_t>();
-    if (invert_first) {
-      int rc = xhe_invert(key, dc.as<uint32_t>(), count, dinv.as<uint32_t>(), st.s);
-      if (rc != XHE_OK) return rc;
-      base = dinv.as<uint32_t>();
-    }
-    int rc = xhe_powmod(key, base, dk.as<uint32_t>(), kw, kbits, count, dout.as<uint32_t>(), st.s);
-    if (rc != XHE_OK) return rc;
-    HIPCHK(hipMemcpyAsync(out, dout.p, cw, hipMemcpyDeviceToHost, st.s));
-    HIPCHK(hipStreamSynchronize(st.s));
-    return XHE_OK;
+    const size_t cb = (size_t)key->n2w * 4;
+    const int64_t chunk = 1 << 16, cmax = std::min<int64_t>(chunk, count);
+    std::unique_ptr<DevBuf> dinv[3];
+    return host_pipeline(
+        key, count, chunk, {{c, cb}, {k, (size_t)kw * 4}}, {{out, cb}},
+        [&](int b, int64_t, int64_t n, void* const* din, void* const* dout, hipStream_t s) -> int {
+          const uint32_t* base = (const uint32_t*)din[0];
+          if (invert_first) {
+            if (!dinv[b]) dinv[b].reset(new DevBuf((size_t)cmax * cb, s));
+            int rc = xhe_invert(key, base, n, dinv[b]->as<uint32_t>(), s);
+            if (rc != XHE_OK) return rc;
+            base = dinv[b]->as<uint32_t>();
+          }
+          return xhe_powmod(key, base, (const uint32_t*)din[1], kw, kbits, n, (uint32_t*)dout[0], s);
+        });
   });
 }
 
