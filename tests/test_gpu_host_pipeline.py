@@ -1,6 +1,6 @@
 """Host-buffer entry points (include/xhe.h *_host) run element-chunked through
-the pinned pipeline (xhe.hip host_pipeline: 64 k / 128 k-element chunks,
-compute stream + one copy stream per direction). Each is checked bit-exactly
+the pinned pipeline (xhe.hip host_pipeline: 64 k - 256 k-element chunks,
+per-slot streams, serialised kernels). Each is checked bit-exactly
 against the same operation on device-resident buffers, at batch sizes that
 cross several chunk boundaries and leave a ragged last chunk - the chunking
 must be invisible (paillier.py:79-123, 156-187, 273-287, 341-398 semantics
@@ -53,7 +53,7 @@ def _dev(torch, a):
 
 def test_encrypt_words_and_raw_host(env):
     nat, L, dk, torch = env
-    n = 150_001
+    n = 300_001  # 128 k chunks (encrypt_host) and 256 k chunks (words_host), ragged ends
     m, r, c = _cipher(env, n, 11)
     out = np.empty((n, dk.n2w), np.uint32)
     nat.check(L.xhe_encrypt_host(dk.handle, vp(m), vp(r), n, vp(out)), "encrypt_host")

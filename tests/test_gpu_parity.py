@@ -60,8 +60,8 @@ def test_decrypt_bit_exact(fx, case):
 
 
 def test_host_encrypt_chunking_is_invisible():
-    """xhe_encrypt_f64_host pipelines 128k-element chunks (compute stream +
-    copy streams, pinned staging); the
+    """xhe_encrypt_f64_host pipelines 256k-element chunks (per-slot streams,
+    pinned staging); the
     randomness is drawn at global element positions, so the result equals one
     device-resident encode + draw + encrypt of the whole batch, and spot
     elements equal the oracle's encryption with the drawn a."""
@@ -74,7 +74,7 @@ def test_host_encrypt_chunking_is_invisible():
     dk = _dkey(g)
     ok = _okey(g)
     L = nat.lib()
-    n = 200_003
+    n = 600_003  # three chunks, the last one ragged
     x = np.random.default_rng(3).standard_normal(n)
     seed, nonce = bytes(range(32)), 77
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
@@ -95,7 +95,7 @@ def test_host_encrypt_chunking_is_invisible():
     torch.cuda.synchronize()
     assert np.array_equal(c.cpu().numpy().view(np.uint32), ct)
     assert np.array_equal(e.cpu().numpy(), ex) and not st.any()
-    for i in (0, 65535, 65536, 131072, n - 1):
+    for i in (0, 262143, 262144, 524288, n - 1):
         mi = O.encode_element(ok, float(x[i]), 7)[0]
         ai = nat.words_to_ints(r[i].cpu().numpy().view(np.uint32))
         assert nat.words_to_ints(ct[i]) == O.encrypt_m(ok, mi, ai)

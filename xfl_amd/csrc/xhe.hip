@@ -1208,7 +1208,7 @@ struct Event {
 // threads copy the results into the caller's buffers. Chunk c + depth - 1 is
 // staged and enqueued before chunk c is drained, so the host copies and both
 // DMA directions overlap the kernels. The kernels of chunk c wait for those of
-// chunk c - 1 (an event): kernels of different chunks never share the CUs (a
+// chunk c - 1 (an event): kernels of different chunks do not share the CUs (a
 // big kernel next to a small one on another stream stretches the small one
 // from microseconds to milliseconds and stalls the chain behind it), while
 // each copy stays in its own stream behind its own kernels, where the runtime
@@ -1220,7 +1220,11 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
                   const std::vector<HostPart>& out, Run&& run) {
   if (count <= 0) return XHE_OK;
   static const bool trace = getenv("XHE_HOST_TRACE") != nullptr;  // per-chunk timings to stderr
-  static const bool serial = getenv("XHE_HOST_SERIAL") != nullptr;  // chunk kernels one after another (A/B)
+  // Kernels of consecutive chunks run one after another ($XHE_HOST_OVERLAP
+  // lets them overlap instead: then the three streams' chunks advance in
+  // lockstep - each one's small kernels wait for CU slots behind the others'
+  // big ones - and the copy-out comes in bursts; 17.6-18.8 vs 19.5-20.4 M/s).
+  static const bool serial = getenv("XHE_HOST_OVERLAP") == nullptr;
   chunk = std::max<int64_t>(1, std::min(chunk, count));
   const int64_t nch = (count + chunk - 1) / chunk;
   const int D = (int)std::min<int64_t>(nch, 3);
@@ -1581,10 +1585,12 @@ int xhe_encrypt_f64_host(const xhe_key* key, const double* x, int64_t count, int
       return fail(XHE_EINVAL, "xhe_encrypt_f64_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    // chunks of 128 k elements (2,048 waves: one full round of the chip) through
-    // host_pipeline; the randomness is drawn at global element positions, so
-    // the ciphertexts do not depend on the chunking
-    const int64_t chunk = host_chunk(1 << 17), cmax = std::min<int64_t>(chunk, count);
+    // chunks of 256 k elements through host_pipeline (with the kernels of
+    // consecutive chunks serialised, a chunk's last partial round of waves is
+    // idle time: 128 k chunks ran 21.8 M/s device-resident, 256 k 25.8 M/s,
+    // tools/chunk_rate.py); the randomness is drawn at global element
+    // positions, so the ciphertexts do not depend on the chunking
+    const int64_t chunk = host_chunk(1 << 18), cmax = std::min<int64_t>(chunk, count);
     std::unique_ptr<DevBuf> dm[3], dr[3];
     return host_pipeline(
         key, count, chunk, {{x, 8}}, {{ct, (size_t)key->n2w * 4}, {exps, 4}, {status, 4}},
@@ -1610,7 +1616,7 @@ int xhe_encrypt_words_host(const xhe_key* key, const uint32_t* m, int64_t count,
       return fail(XHE_EINVAL, "xhe_encrypt_words_host: null argument");
     if (count <= 0) return XHE_OK;
     DevGuard dg(key->device);
-    const int64_t chunk = host_chunk(1 << 17), cmax = std::min<int64_t>(chunk, count);
+    const int64_t chunk = host_chunk(1 << 18), cmax = std::min<int64_t>(chunk, count);
     std::unique_ptr<DevBuf> dr[3];
     return host_pipeline(
         key, count, chunk, {{m, (size_t)key->nw * 4}}, {{ct, (size_t)key->n2w * 4}},
