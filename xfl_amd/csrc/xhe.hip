@@ -1101,12 +1101,14 @@ struct Stream {
   }
 };
 
-// The stream-ordered allocator (hipMallocAsync, every call's workspaces)
-// returns freed memory to the device at each synchronisation by default
-// (release threshold 0), so a host-buffer call that syncs per chunk would map
-// fresh pages for every chunk's workspace. Keep up to kPoolKeep bytes cached
-// in the device's default pool instead (set once per device, at key creation).
-constexpr uint64_t kPoolKeep = 16ull << 30;
+// The stream-ordered allocator (hipMallocAsync, the entry points'
+// workspaces) returns freed memory to the device at each synchronisation by
+// default (release threshold 0), so every synchronised call would map its
+// workspaces afresh. Keep up to kPoolKeep bytes cached in the device's
+// default pool instead (set once per device, at key creation) - small next to
+// the tables, so HBM stays available to the caller (torch's allocator does not
+// draw from this pool).
+constexpr uint64_t kPoolKeep = 2ull << 30;
 void keep_pool_memory(int device) {
   static std::mutex mu;
   static bool done[64] = {};
