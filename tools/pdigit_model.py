@@ -1,0 +1,184 @@
+"""Limb-level model of arithmetic mod P^2 in base-P digits (DESIGN.md §4,
+"Next: arithmetic mod p^2 in base-p digits"): x = x0 + P x1, 0 <= x0, x1 < P,
+
+    (x0 + P x1)(y0 + P y1) = d0 + P ((d1 + x0 y1 + x1 y0) mod P)   (mod P^2)
+    with x0 y0 = d0 + P d1, split by Barrett reduction (HAC 14.42) in
+    radix b = 2^28 with a truncated quotient product.
+
+It follows the schedule a kernel would run - 64-bit lazy column sums of 28-bit
+limbs, one carry normalisation per product - checks every result against
+Python integers, checks that no column sum reaches 2^64, and counts the
+32x32->64 multiply-adds (v_mad_u64_u32) per product and per squaring next to
+the current Montgomery product mod P^2 (2 S^2 + S, S = 74).
+
+    python tools/pdigit_model.py [--bits 2048] [--trials 300]
+"""
+import argparse
+import json
+import random
+
+W = 28
+B = 1 << W
+MASK = B - 1
+
+
+def limbs(x, n):
+    out = [(x >> (W * i)) & MASK for i in range(n)]
+    assert x >> (W * n) == 0, "value does not fit"
+    return out
+
+
+def value(l):
+    return sum(v << (W * i) for i, v in enumerate(l))
+
+
+class Counter:
+    def __init__(self):
+        self.mads = 0
+        self.max_col = 0
+
+
+def cols_mul(a, b, ctr, lo=0, hi=None, acc=None):
+    """lazy column sums of a*b for columns lo..hi-1 (hi default: all)"""
+    n = len(a) + len(b) - 1
+    hi = n if hi is None else hi
+    acc = acc if acc is not None else [0] * (hi - lo)
+    for i, ai in enumerate(a):
+        for j, bj in enumerate(b):
+            c = i + j
+            if lo <= c < hi:
+                acc[c - lo] += ai * bj
+                ctr.mads += 1
+    ctr.max_col = max(ctr.max_col, max(acc) if acc else 0)
+    return acc
+
+
+def normalize(cols, n, wrap=False):
+    """carry-propagate lazy columns into n limbs (wrap: modulo b^n)"""
+    out, carry = [], 0
+    for i in range(n):
+        x = (cols[i] if i < len(cols) else 0) + carry
+        out.append(x & MASK)
+        carry = x >> W
+    assert wrap or carry == 0, "normalisation overflow"
+    return out
+
+
+class Digits:
+    """Z/P^2 Z in base-P digits with Barrett reduction by P."""
+
+    def __init__(self, P):
+        self.P = P
+        self.k = -(-P.bit_length() // W)          # limbs of P (37 at 1024 bits)
+        self.Pl = limbs(P, self.k)
+        self.mu = (1 << (W * 2 * self.k)) // P     # floor(b^2k / P)
+        self.mul_ = limbs(self.mu, self.k + 1)
+
+    def barrett(self, T, ctr, want_q):
+        """(q, r) with T = q P + r, 0 <= r < P, for T < b^2k given as 2k limbs.
+        q3 from the columns >= k-1 of q1*mu only (truncated): q - q3 <= 3."""
+        k = self.k
+        assert len(T) == 2 * k and value(T) < B ** (2 * k)
+        q1 = T[k - 1:]                                     # floor(T / b^(k-1)): k+1 limbs
+        top = cols_mul(q1, self.mul_, ctr, lo=k - 1)       # columns k-1 .. 2k+1
+        # top[i] is column k-1+i: floor(q1 mu / b^(k+1)) = floor(v / b^2)
+        v = sum(c << (W * i) for i, c in enumerate(top))
+        q3 = v >> (2 * W)
+        q3l = limbs(q3, k + 1)
+        r2 = normalize(cols_mul(q3l, self.Pl, ctr, hi=k + 1), k + 1, wrap=True)  # (q3 P) mod b^(k+1)
+        r = value(T[:k + 1]) - value(r2)
+        if r < 0:
+            r += B ** (k + 1)
+        q, fix = q3, 0
+        while r >= self.P:
+            r -= self.P
+            q += 1
+            fix += 1
+        assert fix <= 3, f"Barrett needed {fix} corrections"
+        ctr.fix = max(getattr(ctr, "fix", 0), fix)
+        return (q if want_q else None), r
+
+    def split(self, x):
+        return x % self.P, x // self.P
+
+    def mul(self, x, y, ctr):
+        (x0, x1), (y0, y1) = x, y
+        k = self.k
+        a0, a1, b0, b1 = (limbs(v, k) for v in (x0, x1, y0, y1))
+        T = normalize(cols_mul(a0, b0, ctr), 2 * k)
+        d1, d0 = self.barrett(T, ctr, True)
+        U = cols_mul(a0, b1, ctr)
+        U = cols_mul(a1, b0, ctr, acc=U)
+        U = [u + dl for u, dl in zip(U, limbs(d1, k) + [0] * len(U))]
+        ctr.max_col = max(ctr.max_col, max(U))
+        U = normalize(U, 2 * k)
+        _, z1 = self.barrett(U, ctr, False)
+        return d0, z1
+
+    def sqr(self, x, ctr):
+        x0, x1 = x
+        k = self.k
+        a0, a1 = limbs(x0, k), limbs(x1, k)
+        # x0^2 by product scanning: i < j pairs doubled, plus the squares
+        cols = [0] * (2 * k - 1)
+        for i in range(k):
+            for j in range(i, k):
+                cols[i + j] += a0[i] * a0[j] * (1 if i == j else 2)
+                ctr.mads += 1
+        ctr.max_col = max(ctr.max_col, max(cols))
+        T = normalize(cols, 2 * k)
+        d1, d0 = self.barrett(T, ctr, True)
+        U = cols_mul(a0, a1, ctr)
+        U = [2 * u + dl for u, dl in zip(U, limbs(d1, k) + [0] * len(U))]
+        ctr.max_col = max(ctr.max_col, max(U))
+        U = normalize(U, 2 * k)
+        _, z1 = self.barrett(U, ctr, False)
+        return d0, z1
+
+
+def random_prime_like(bits, rng):
+    """an odd number with the top bit set (primality is irrelevant to the
+    arithmetic being modelled)"""
+    return rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bits", type=int, default=2048, help="key size; P has bits/2 bits")
+    ap.add_argument("--trials", type=int, default=300)
+    args = ap.parse_args()
+    rng = random.Random(1)
+    res = {"bits": args.bits}
+    worst_col = 0
+    fix = 0
+    for t in range(args.trials):
+        P = random_prime_like(args.bits // 2, rng)
+        D = Digits(P)
+        P2 = P * P
+        edge = [0, 1, P2 - 1, P2 - P, P - 1, P]
+        x = edge[t % len(edge)] if t < 12 else rng.randrange(P2)
+        y = edge[(t // 2) % len(edge)] if t < 12 else rng.randrange(P2)
+        cm, cs = Counter(), Counter()
+        z = D.mul(D.split(x), D.split(y), cm)
+        assert z[0] + P * z[1] == x * y % P2
+        s = D.sqr(D.split(x), cs)
+        assert s[0] + P * s[1] == x * x % P2
+        worst_col = max(worst_col, cm.max_col, cs.max_col)
+        fix = max(fix, getattr(cm, "fix", 0), getattr(cs, "fix", 0))
+        res["mads_per_product"] = cm.mads
+        res["mads_per_squaring"] = cs.mads
+        res["k_limbs"] = D.k
+    S = -(-args.bits // W)
+    res["montgomery_mod_P2_mads"] = 2 * S * S + S
+    res["montgomery_square_mads"] = S * (S + 1) // 2 + S * S + S
+    res["product_ratio"] = res["mads_per_product"] / res["montgomery_mod_P2_mads"]
+    res["squaring_ratio"] = res["mads_per_squaring"] / res["montgomery_square_mads"]
+    res["max_column_sum_log2"] = worst_col.bit_length()
+    res["max_barrett_corrections"] = fix
+    res["trials_bit_exact"] = args.trials
+    assert worst_col < (1 << 64)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
