@@ -103,7 +103,12 @@ def lib():
                 pass
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
-                fn = getattr(L, name)
+                try:
+                    fn = getattr(L, name)
+                except AttributeError:
+                    if "XHE_LIB" in os.environ:  # an older A/B build: bind what it has
+                        continue
+                    raise
                 fn.restype = res
                 fn.argtypes = args
             _lib = L

@@ -1108,12 +1108,15 @@ struct Stream {
 // default pool instead (set once per device, at key creation) - small next to
 // the tables, so HBM stays available to the caller (torch's allocator does not
 // draw from this pool).
-constexpr uint64_t kPoolKeep = 2ull << 30;
+#ifndef XHE_POOL_KEEP_MB
+#define XHE_POOL_KEEP_MB 2048
+#endif
+constexpr uint64_t kPoolKeep = (uint64_t)XHE_POOL_KEEP_MB << 20;
 void keep_pool_memory(int device) {
   static std::mutex mu;
   static bool done[64] = {};
   std::lock_guard<std::mutex> g(mu);
-  if (device < 0 || device >= 64 || done[device]) return;
+  if (device < 0 || device >= 64 || done[device] || kPoolKeep == 0) return;
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
     uint64_t keep = kPoolKeep;
@@ -1236,20 +1239,28 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
   for (auto& h : in) parts.push_back(h.elem_bytes * chunk), per_chunk += h.elem_bytes * chunk;
   for (auto& h : out) parts.push_back(h.elem_bytes * chunk), per_chunk += h.elem_bytes * chunk;
   const bool staged = per_chunk >= ((size_t)1 << 20);
-  Stream st[3];
-  Event ev_k[3];
+  // only as many streams/events as slots: a one-chunk call (small batches:
+  // the LR operators' per-batch calls) pays for one stream, as a plain call
+  std::vector<std::unique_ptr<Stream>> st_;
+  std::vector<std::unique_ptr<Event>> ev_;
+  for (int b = 0; b < D; ++b) {
+    st_.emplace_back(new Stream());
+    ev_.emplace_back(new Event());
+  }
+  auto st = [&](int b) -> Stream& { return *st_[b]; };
+  auto ev_k = [&](int b) -> Event& { return *ev_[b]; };
   WsCache wsc[3];  // destroyed before the streams (frees are stream-ordered)
-  for (int b = 0; b < 3; ++b) wsc[b].s = st[b].s;
+  for (int b = 0; b < D; ++b) wsc[b].s = st(b).s;
   std::vector<std::unique_ptr<DevBuf>> dev;  // [slot][part]
   for (int b = 0; b < D; ++b)
-    for (size_t k = 0; k < parts.size(); ++k) dev.emplace_back(new DevBuf(parts[k], st[b].s));
+    for (size_t k = 0; k < parts.size(); ++k) dev.emplace_back(new DevBuf(parts[k], st(b).s));
   std::unique_ptr<PinnedSlots> pin;
   if (staged) pin.reset(new PinnedSlots(key->device, D, parts));
   auto dptr = [&](int b, int k) { return dev[(size_t)b * parts.size() + k]->p; };
   auto enqueue = [&](int64_t c) -> int {
     const int b = (int)(c % D);
     const int64_t off = c * chunk, n = std::min(chunk, count - off);
-    hipStream_t s = st[b].s;
+    hipStream_t s = st(b).s;
     const auto tin = std::chrono::steady_clock::now();
     std::vector<void*> din(ni), dout(no);
     for (int k = 0; k < ni; ++k) {
@@ -1266,7 +1277,7 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
     if (trace)
       fprintf(stderr, "[host_pipeline] chunk %lld: staged inputs %.3f ms\n", (long long)c,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tin).count());
-    if (serial && c > 0) HIPCHK(hipStreamWaitEvent(s, ev_k[(c - 1) % D].e, 0));
+    if (serial && c > 0) HIPCHK(hipStreamWaitEvent(s, ev_k((int)((c - 1) % D)).e, 0));
     for (int k = 0; k < no; ++k) dout[k] = out[k].host ? dptr(b, ni + k) : nullptr;
     const auto tr = std::chrono::steady_clock::now();
     for (auto& w : wsc[b].blk) w.used = false;
@@ -1280,7 +1291,7 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
     }
     t_ws = nullptr;
     if (rc != XHE_OK) return rc;
-    HIPCHK(hipEventRecord(ev_k[b].e, s));
+    HIPCHK(hipEventRecord(ev_k(b).e, s));
     const auto td = std::chrono::steady_clock::now();
     for (int k = 0; k < no; ++k)
       if (out[k].host) {
@@ -1303,7 +1314,7 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
     const int b = (int)(c % D);
     const int64_t off = c * chunk, n = std::min(chunk, count - off);
     const auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(hipStreamSynchronize(st[b].s));
+    HIPCHK(hipStreamSynchronize(st(b).s));
     const auto t1 = std::chrono::steady_clock::now();
     if (staged)
       for (int k = 0; k < no; ++k)
