@@ -238,6 +238,9 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
     # (logistic_regression/label_trainer.py:193-199, 258); the context uses
     # this run's key handle (same tables)
     from xfl_amd.paillier import Paillier, PaillierContext
+    # one GPU's rates: the drop-in would otherwise spread each call over every
+    # visible GPU (num_cores=-1, the reference's default), e.g. all 8 of a node
+    os.environ["XHE_DEVICES"] = str(dk.device)
     ctx = PaillierContext().init(p_, q_, djn_h_pow_n=h_)
     ctx._dev = {dk.device: dk}
     x32 = xh.astype(np.float32)
