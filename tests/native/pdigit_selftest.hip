@@ -45,10 +45,12 @@ __global__ void __launch_bounds__(256, 2) k_check(const uint32_t* P, const uint3
   }
 }
 
-// ITER products of each lane's residue with its own fixed second operand
+// ITER products (MODE 0) or squarings (MODE 1) of each lane's residue with its
+// own fixed second operand (one kernel per mode: registers are allocated for
+// that code path alone)
+template <int MODE>
 __global__ void __launch_bounds__(256, 2) k_time_digit(const uint32_t* P, const uint32_t* MU, const uint32_t* x,
-                                                       const uint32_t* y, uint32_t* out, int count, int iters,
-                                                       int mode) {
+                                                       const uint32_t* y, uint32_t* out, int count, int iters) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
   PD D{P, MU};
@@ -62,7 +64,7 @@ __global__ void __launch_bounds__(256, 2) k_time_digit(const uint32_t* P, const 
     y1[i] = y[(size_t)s * 2 * K + K + i];
   }
   for (int t = 0; t < iters; ++t) {
-    if (mode == 0) D.mul(x0, x1, y0, y1);
+    if constexpr (MODE == 0) D.mul(x0, x1, y0, y1);
     else D.sqr(x0, x1);
   }
   uint32_t acc = 0;
@@ -215,10 +217,10 @@ int main() {
     hipLaunchKernelGGL(k_time_mont, dim3(lanes / 256), dim3(256), 0, 0, dN, n0, dmx, dmy, dsink, lanes, iters);
   });
   const double dmul = time_it([&] {
-    hipLaunchKernelGGL(k_time_digit, dim3(lanes / 256), dim3(256), 0, 0, dP, dMU, dx, dy, dsink, lanes, iters, 0);
+    hipLaunchKernelGGL(k_time_digit<0>, dim3(lanes / 256), dim3(256), 0, 0, dP, dMU, dx, dy, dsink, lanes, iters);
   });
   const double dsqr = time_it([&] {
-    hipLaunchKernelGGL(k_time_digit, dim3(lanes / 256), dim3(256), 0, 0, dP, dMU, dx, dy, dsink, lanes, iters, 1);
+    hipLaunchKernelGGL(k_time_digit<1>, dim3(lanes / 256), dim3(256), 0, 0, dP, dMU, dx, dy, dsink, lanes, iters);
   });
   printf("{\"products_per_s\": {\"montgomery_mod_P2\": %.4g, \"digit_mul\": %.4g, \"digit_sqr\": %.4g}, "
          "\"digit_mul_vs_montgomery\": %.3f, \"lanes\": %d, \"iters\": %d}\n",
