@@ -1,0 +1,43 @@
+"""Device arithmetic self-tests on the GPU (binaries built on the CPU by
+tests/native/build.py, called from __graft_entry__.build()):
+
+* mont_selftest - Mont<S, W, TPI>::mul / reduce_once / normalize for every
+  limb shape of every key size against host big integers (hostbn.hpp);
+* pdigit_selftest - the base-P digit arithmetic mod P^2 (pdigit_dev.hpp,
+  DESIGN.md §4) against host big integers, plus its timing line.
+
+Each binary prints one JSON line per check with the number of mismatching
+elements; all must be 0."""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "native", "_build")
+
+
+def _run(name):
+    exe = os.path.join(BUILD, name)
+    if not os.path.exists(exe):
+        pytest.skip(f"{name} not built (python tests/native/build.py)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    checks = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{") and '"bad"' in l]
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert checks and all(c["bad"] == 0 for c in checks), checks
+    return checks, r.stdout
+
+
+def test_montgomery_shapes_selftest():
+    checks, _ = _run("mont_selftest")
+    assert len(checks) >= 9
+
+
+def test_base_p_digit_selftest():
+    checks, out = _run("pdigit_selftest")
+    assert {c["check"] for c in checks} == {"mul", "sqr"}
+    assert all(c["of"] == 4096 for c in checks)
+    assert "products_per_s" in out
