@@ -79,7 +79,10 @@ int xhe_decode(const xhe_key* key, const uint32_t* m_dev, const int32_t* exp_dev
 /* Ciphertext addition PaillierCiphertext._add_encrypted (paillier.py:106-123,
  * 79-86, 153-154): out = a' * b' mod n^2 where the operand with the larger
  * exponent is first raised to 2^(e - min(ea, eb)); eout = min(ea, eb).
- * ea/eb may be NULL (all 0). dmax >= max |ea - eb| bounds the squarings. */
+ * ea/eb may be NULL (all 0). dmax >= max |ea - eb| bounds the squarings.
+ * As in the reference, a gap d with 2^d >= min_value_for_negative (d >=
+ * ~bitlen(n) - 1) takes _raw_mul's negative branch: that operand is raised to
+ * 2^d - n instead (paillier.py:79-86, 173-187; same plaintext, other bits). */
 int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev, const uint32_t* b_dev,
                const int32_t* eb_dev, int64_t count, int dmax, uint32_t* out_dev, int32_t* eout_dev, void* stream);
 /* PaillierCiphertext._raw_mul positive branch (paillier.py:156-187):
@@ -95,7 +98,12 @@ int xhe_invert(const xhe_key* key, const uint32_t* c_dev, int64_t count, uint32_
  * out[s] = prod_{i in [seg_begin[s], seg_begin[s+1])} c_i^(2^d_i) mod n^2,
  * d_i = e_i - (min exponent of the segment) (NULL = all 0), dmax >= max d_i.
  * seg_begin is a HOST array of nseg+1 offsets into the segment-ordered input;
- * an empty segment yields 1 (the encryption of 0 without obfuscation). */
+ * an empty segment yields 1 (the encryption of 0 without obfuscation).
+ * This is the order-free fold: equal to any order of the reference's
+ * pairwise adds while every gap is below the negative-branch threshold
+ * (see xhe_mulmod); past it the reference's bits depend on the addition tree,
+ * and the caller pre-aligns those elements (xfl_amd/paillier/ops.py
+ * segment_sums_words). */
 int xhe_segprod(const xhe_key* key, const uint32_t* c_dev, const int32_t* d_dev, int dmax, int64_t count,
                 const int64_t* seg_begin, int64_t nseg, uint32_t* out_dev, void* stream);
 

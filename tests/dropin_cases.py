@@ -242,3 +242,44 @@ def encrypt_decrypt_shapes(fx):
     obj = np.asarray(Paillier.encrypt(pub, x[0], precision=7))
     assert obj.dtype == object and np.all(np.abs(Paillier.decrypt(priv, obj) - x[0]) < 1e-4)
     assert np.all(np.abs(Paillier.decrypt(priv, Paillier.obfuscate(obj)) - x[0]) < 1e-4)
+
+
+def gap_alignment(fx, vectorized):
+    """Adds across alignment gaps that take _raw_mul's negative branch
+    (1 << d >= min_value_for_negative: c^(2^d - n), paillier.py:79-86,
+    173-187), bit-exact vs the reference: the operands (a product with two
+    2^-960 scalars), element-wise adds with the public and the private
+    context, np.sum (numpy's left fold) and Python's sum() in four orders."""
+    from xfl_amd.paillier import PaillierArray
+    g = load_fixture(fx)
+    priv, pub = ctxs(g)
+    ops = g["ops"]
+    want = lambda name: ([hx(r) for r in ops[name]["raw"]], ops[name]["exp"])  # noqa: E731
+    cg = cts(pub, ops["gap"])
+    scale = fl(ops["gap"]["scale"])
+    if vectorized:
+        A = PaillierArray(cg)
+        first = A[:1] * scale * scale
+        assert raw(first) == ([want("gap_operands")[0][0]], [want("gap_operands")[1][0]])
+    else:
+        gc = np.array([cg[0] * scale * scale] + list(cg[1:]), dtype=object)
+        assert raw(gc) == want("gap_operands")
+    pairs = ops["gap"]["pairs"]
+    li, ri = [i for i, _ in pairs], [j for _, j in pairs]
+    for name, ctx in (("pub", pub), ("priv", priv)):
+        gc = cts(ctx, ops["gap_operands"])
+        if vectorized:
+            A = PaillierArray(gc)
+            got = A[li] + A[ri]
+        else:
+            got = np.array([gc[i] + gc[j] for i, j in pairs], dtype=object)
+        assert raw(got) == want(f"gap_add_{name}"), name
+    gc = cts(pub, ops["gap_operands"])
+    orders = ops["gap_sum"]["orders"]
+    if vectorized:
+        A = PaillierArray(gc)
+        sums = [np.sum(A[o]) for o in orders]
+    else:
+        sums = [np.sum(gc[o]) for o in orders]
+    assert raw(np.array(sums, dtype=object)) == want("gap_sum")
+    assert raw(np.array([sum(gc[o]) for o in orders], dtype=object)) == want("gap_pyfold")

@@ -263,6 +263,29 @@ def gen_key_fixture(bits, djn, seed, n_vec):
     # Wire format: pickle of RawCiphertext objects (paillier.py:244-258), uncompressed.
     ops["wire_a4"] = Paillier.serialize(ca[:4], compression=False).hex()
     ops["wire_ctx_pub"] = pub.serialize().hex()
+    if bits == 2048:
+        # Alignment across gaps of ~bitlen(n) exponent steps:
+        # _decrease_exponent_to's scalar 1 << d reaches min_value_for_negative
+        # and _raw_mul takes its negative branch (paillier.py:79-86, 173-187).
+        # Encoded floats have exponents in [-1023, 0] (a float scalar at
+        # precision None as well), so the small operand is a product: Enc(1.0) *
+        # 2^-960 * 2^-960, exponent -2076. Exponents of gc: -2076, -31, -30, -29,
+        # -28, -36, 0, -49 (gaps to gc[0]: 2045 .. 2048, 2040, 2076, 2027).
+        gx = np.array([1.0, 2.0 ** 21, -1.5 * 2.0 ** 22, 2.0 ** 23, 2.0 ** 24, -(2.0 ** 16), 1.5 * 2.0 ** 52, 12.5],
+                      dtype=np.float64)
+        scale = 2.0 ** -960
+        _, cg = encrypt_case(pub, gx, None, kind="f64")
+        gc = np.array([cg[0] * scale * scale] + list(cg[1:]), dtype=object)
+        gcp = Paillier.ciphertext_from(priv, Paillier.serialize(gc, compression=False), compression=False)
+        pairs = [(0, 1), (1, 0), (0, 2), (0, 3), (3, 0), (0, 4), (0, 5), (5, 0), (0, 6), (0, 7), (7, 7), (1, 6)]
+        ops["gap"] = dict(cts(cg), input=[F(v) for v in gx], scale=F(scale), pairs=pairs,
+                          dneg=(int(priv.min_value_for_negative) - 1).bit_length())
+        ops["gap_operands"] = cts(gc)
+        ops["gap_add_pub"] = cts(np.array([gc[i] + gc[j] for i, j in pairs], dtype=object))
+        ops["gap_add_priv"] = cts(np.array([gcp[i] + gcp[j] for i, j in pairs], dtype=object))
+        orders = [[6, 5, 0, 7, 2], [6, 0, 4, 1], [3, 6, 0, 2], [0, 6, 1]]
+        ops["gap_sum"] = dict(cts(np.array([np.sum(gc[o]) for o in orders], dtype=object)), orders=orders)
+        ops["gap_pyfold"] = cts(np.array([sum(gc[o]) for o in orders], dtype=object))
     return out
 
 

@@ -117,16 +117,14 @@ def powmod_words(ctx, cw, kw_, kbits, invert_first=False, num_cores=-1):
     return _w(out, 2 * _nw(ctx))
 
 
-def segment_sums_words(ctx, cw, exps, seg_begin):
+def segprod_words(ctx, cw, d, seg):
     k = _key(ctx)
-    raws, e = _i(cw), np.asarray(exps).tolist()
-    out, eo = [], []
-    for s in range(len(seg_begin) - 1):
-        lo, hi = int(seg_begin[s]), int(seg_begin[s + 1])
-        r, m = O.sum_ct(k, raws[lo:hi], e[lo:hi]) if hi > lo else (1, 0)
-        out.append(r)
-        eo.append(m)
-    return _w(out, 2 * _nw(ctx)), np.array(eo, dtype=np.int32)
+    raws, dd = _i(cw), np.asarray(d).tolist()
+    out = []
+    for s in range(len(seg) - 1):
+        lo, hi = int(seg[s]), int(seg[s + 1])
+        out.append(O.sum_ct(k, raws[lo:hi], dd[lo:hi])[0] if hi > lo else 1)
+    return _w(out, 2 * _nw(ctx))
 
 
 def multiexp_words(ctx, bw, idx, kw_, kbits, win_bits=0):
@@ -144,7 +142,7 @@ def multiexp_words(ctx, bw, idx, kw_, kbits, win_bits=0):
 
 
 NAMES = ["encrypt_floats_words", "encrypt_encoded_words", "decrypt_words", "decrypt_decode_words", "add_words",
-         "powmod_words", "segment_sums_words", "multiexp_words"]
+         "powmod_words", "segprod_words", "multiexp_words"]
 
 
 def install(monkeypatch):

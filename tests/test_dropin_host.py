@@ -84,10 +84,17 @@ def test_sharded_slices_cover_the_batch(monkeypatch):
         devs = [int(d) for d in spec.split(",")]
         assert [s[0] for s in seen] == devs[:want_k]
     monkeypatch.delenv("XHE_DEVICES")
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
     monkeypatch.setattr("xfl_amd._native.visible_devices", lambda: 8)
-    assert PaillierContext.shard_devices(-1) == list(range(8))
+    # default: the process's own GPU only (no key/tables on the other GPUs)
+    assert PaillierContext.shard_devices(-1) == [0]
     assert PaillierContext.shard_devices(3) == [0, 1, 2]
     assert PaillierContext.shard_devices(1) == [0]
+    monkeypatch.setenv("LOCAL_RANK", "6")
+    assert PaillierContext.shard_devices(-1) == [6]
+    assert PaillierContext.shard_devices(3) == [6, 7, 0]
+    monkeypatch.setenv("XHE_DEVICES", "all")
+    assert PaillierContext.shard_devices(-1) == list(range(8))
 
 
 def test_table_window_policy(monkeypatch):
@@ -100,7 +107,9 @@ def test_table_window_policy(monkeypatch):
 
     class FakeKey:
         def __init__(self, bits, n, p=None, q=None, h=None, device=0, win_bits=0):
-            self.win_bits = win_bits if (p is not None and h) else 0
+            wb = win_bits if (p is not None and h) else 0
+            self.win_bits = wb & 0xFF
+            self.win_split = bool(wb & 0x100)
             built.append((device, self.win_bits))
 
     monkeypatch.setattr(nat, "DeviceKey", FakeKey)
@@ -124,6 +133,19 @@ def test_table_window_policy(monkeypatch):
     monkeypatch.setenv("XHE_WIN_BITS", "12")
     priv.set_device_window(None)
     assert priv.device_key().win_bits == 12
+    # split layouts: the masked window and the layout flag compare separately,
+    # so a built split key is reused, not rebuilt on every call
+    from xfl_amd._native import XHE_WIN_SPLIT
+    n_before = len(built)
+    priv.set_device_window("18s")
+    k1 = priv.device_key()
+    assert k1.win_bits == 18 and k1.win_split
+    assert priv.device_key() is k1 and len(built) == n_before + 1
+    priv.set_device_window(18 | XHE_WIN_SPLIT)
+    assert priv.device_key().win_split and len(built) == n_before + 2
+    monkeypatch.setenv("XHE_WIN_BITS", "14s")
+    priv.set_device_window(None)
+    assert priv.device_key().win_bits == 14 and priv.device_key().win_split
     assert pub.device_key().win_bits == 0
     nodjn, _ = C.ctxs(load_fixture("paillier_2048_nodjn.json"))
     assert nodjn.device_key().win_bits == 0
@@ -151,3 +173,9 @@ def test_window_layouts():
     assert bench.pick_window(2048, 230 * 10**9, split=True) == 23  # 240.5 GB + 16 GiB does not fit
     assert bench.pick_window(3072, 287 * 10**9, split=True) == 22
     assert bench.pick_window(4096, 287 * 10**9) == 21
+
+
+@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_gap_alignment_negative_branch(fx, vectorized):
+    C.gap_alignment(fx, vectorized)

@@ -28,6 +28,43 @@ def test_histogram_groupby_bit_exact():
     C.histogram_groupby(FIXTURES[0])
 
 
+@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("fx", ["paillier_2048_djn.json", "paillier_2048_nodjn.json"])
+def test_gap_alignment_negative_branch(fx, vectorized):
+    """device alignment across gaps >= the negative-branch threshold:
+    xhe_mulmod's fix-up (vectorized adds) and the tree-aware segmented
+    product (np.sum, Python sum, deferred object adds)"""
+    C.gap_alignment(fx, vectorized)
+
+
+def test_mulmod_gap_c_abi():
+    """xhe_mulmod itself (device buffers) reproduces _raw_mul's negative
+    branch for every gap case of the fixture, mixed with small gaps in one call"""
+    import torch
+
+    from xfl_amd import _native as nat
+    g = load_fixture("paillier_2048_djn.json")
+    priv, pub = C.ctxs(g)
+    ops = g["ops"]
+    dk = pub.device_key()
+    ops_raw = [hx(r) for r in ops["gap_operands"]["raw"]]
+    ops_exp = ops["gap_operands"]["exp"]
+    pairs = ops["gap"]["pairs"]
+    a = torch.from_numpy(nat.ints_to_words([ops_raw[i] for i, _ in pairs], dk.n2w).view(np.int32).copy()).cuda()
+    b = torch.from_numpy(nat.ints_to_words([ops_raw[j] for _, j in pairs], dk.n2w).view(np.int32).copy()).cuda()
+    ea = torch.tensor([ops_exp[i] for i, _ in pairs], dtype=torch.int32).cuda()
+    eb = torch.tensor([ops_exp[j] for _, j in pairs], dtype=torch.int32).cuda()
+    out = torch.empty_like(a)
+    eo = torch.empty_like(ea)
+    dmax = int((ea - eb).abs().max().item())
+    s = torch.cuda.current_stream().cuda_stream
+    nat.check(nat.lib().xhe_mulmod(dk.handle, a.data_ptr(), ea.data_ptr(), b.data_ptr(), eb.data_ptr(), len(pairs),
+                                   dmax, out.data_ptr(), eo.data_ptr(), s), "mulmod")
+    torch.cuda.synchronize()
+    assert nat.words_to_ints(out.cpu().numpy().view(np.uint32)) == [hx(r) for r in ops["gap_add_pub"]["raw"]]
+    assert eo.tolist() == ops["gap_add_pub"]["exp"]
+
+
 @pytest.mark.parametrize("fx", FIXTURES)
 def test_decrypt_matches_reference(fx):
     C.decrypt_matches_reference(fx)

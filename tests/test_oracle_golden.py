@@ -155,3 +155,42 @@ def test_matmul_and_hist(golden):
         members = [i for i, bb in enumerate(h["bins"]) if bb == b]
         assert len(members) == h["count"][idx]
         assert O.sum_ct(kpub, [cr[i] for i in members], [ce[i] for i in members]) == (sr[idx], se[idx])
+
+
+@pytest.mark.parametrize("fx", ["paillier_2048_djn.json", "paillier_2048_nodjn.json"])
+def test_alignment_gap_negative_branch(fx):
+    """Additions whose alignment gap d has 1 << d >= min_value_for_negative
+    (the 2048-bit fixtures' gap cases): _raw_mul's negative branch gives
+    c^(2^d - n) (paillier.py:79-86, 173-187). The oracle's add_ct reproduces
+    the reference's bits for single adds, its left fold those of np.sum and
+    Python's sum (which starts from 0 + x0 = x0 + Enc(0)); the order-free
+    product does not (which is why the device path tracks the addition tree)."""
+    from tests.conftest import load_fixture
+    g = load_fixture(fx)
+    k = _key(g, private=False)
+    ops = g["ops"]
+    assert ops["gap"]["dneg"] == (k["min_value_for_negative"] - 1).bit_length()
+    cr, ce = _cts(ops["gap"])
+    scale = fl(ops["gap"]["scale"])
+    t = O.mul_ct(k, cr[0], ce[0], scale)
+    t = O.mul_ct(k, t[0], t[1], scale)
+    gr, ge = _cts(ops["gap_operands"])
+    assert (gr[0], ge[0]) == t and gr[1:] == cr[1:] and ge[1:] == ce[1:]
+    for name in ("gap_add_pub", "gap_add_priv"):
+        rr, re_ = _cts(ops[name])
+        for idx, (i, j) in enumerate(ops["gap"]["pairs"]):
+            assert O.add_ct(k, gr[i], ge[i], gr[j], ge[j]) == (rr[idx], re_[idx]), (name, i, j)
+    sr, se = _cts(ops["gap_sum"])
+    pr, pe = _cts(ops["gap_pyfold"])
+    differs = 0
+    for idx, o in enumerate(ops["gap_sum"]["orders"]):
+        acc = (gr[o[0]], ge[o[0]])
+        for i in o[1:]:
+            acc = O.add_ct(k, acc[0], acc[1], gr[i], ge[i])
+        assert acc == (sr[idx], se[idx])
+        acc = O.add_ct(k, gr[o[0]], ge[o[0]], 1, 0)  # 0 + x0 -> x0.__radd__(0) = x0 + Enc(0)
+        for i in o[1:]:
+            acc = O.add_ct(k, acc[0], acc[1], gr[i], ge[i])
+        assert acc == (pr[idx], pe[idx])
+        differs += O.sum_ct(k, [gr[i] for i in o], [ge[i] for i in o]) != (sr[idx], se[idx])
+    assert differs >= 1

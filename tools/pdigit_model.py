@@ -136,6 +136,113 @@ class Digits:
         return d0, z1
 
 
+class MontDigits:
+    """Z/P^2 Z in MONTGOMERY digits - the form the device kernel runs
+    (xfl_amd/csrc/pdigit_dev.hpp PMD): with R = b^k (b = 2^28, k limbs of P),
+    a residue x is held as two k-limb integers (a, c) with
+
+        x R^2 = R a + P c   (mod P^2)
+
+    and the product of (a, c) and (e, f) is (a', c') with
+        a' = REDC(a e)                  = (a e + m P) / R
+        c' = REDC(a f + c e) + (R-1-m) + E,   E = (1 - R) mod P
+    where m is the first REDC's quotient (a e = R a' - m P exactly), so that
+    R a' + P c' = (R a + P c)(R e + P f) R^-2 (mod P^2). Both REDCs run as one
+    operand-scanning loop over the limbs of (e, f) with lazy 64-bit
+    accumulators; (R - 1 - m) + E enters limb by limb at the top of the second
+    accumulator (limb i of m is known at step i and lands at weight b^i).
+    Each step: k mads e_i*a + k mads m_i*P (first) and 3k mads e_i*c + f_i*a +
+    m'_i*P (second): 5k^2 per product vs 2(2k)^2 for Montgomery mod P^2."""
+
+    def __init__(self, P):
+        self.P = P
+        self.k = -(-P.bit_length() // W)
+        self.R = 1 << (W * self.k)
+        self.Pl = limbs(P, self.k)
+        self.n0inv = (-pow(P, -1, B)) % B
+        self.E = (1 - self.R) % P
+        self.El = limbs(self.E, self.k)
+
+    def to_form(self, x):
+        """(a, c) with R a + P c = x R^2 mod P^2, a, c < P"""
+        P, R = self.P, self.R
+        X = x * R * R % (P * P)
+        a = X * pow(R, -1, P) % P
+        c = ((X - R * a) // P) % P  # exact: X = R a (mod P)
+        return a, c
+
+    def value(self, a, c):
+        P2 = self.P * self.P
+        return (self.R * a + self.P * c) * pow(self.R, -2, P2) % P2
+
+    def mul(self, x, y, ctr):
+        """one product, as the kernel's step schedule; returns (a', c')"""
+        k, P = self.k, self.P
+        (a, c), (e, f) = x, y
+        al, cl = limbs_loose(a, k), limbs_loose(c, k)
+        el, fl = limbs(e, k), limbs(f, k)
+        T1 = [0] * k
+        T2 = [0] * k
+        for i in range(k):
+            # position 0 first: the quotient digits
+            x1 = T1[0] + el[i] * al[0]
+            m1 = (x1 * self.n0inv) & MASK
+            x1 += m1 * self.Pl[0]
+            x2 = T2[0] + el[i] * cl[0] + fl[i] * al[0]
+            m2 = (x2 * self.n0inv) & MASK
+            x2 += m2 * self.Pl[0]
+            assert x1 & MASK == 0 and x2 & MASK == 0
+            ctr.mads += 5
+            for j in range(1, k):
+                T1[j - 1] = T1[j] + el[i] * al[j] + m1 * self.Pl[j]
+                T2[j - 1] = T2[j] + el[i] * cl[j] + fl[i] * al[j] + m2 * self.Pl[j]
+                ctr.mads += 5
+            T1[k - 1] = 0
+            T2[k - 1] = (MASK - m1) + self.El[i]
+            T1[0] += x1 >> W
+            T2[0] += x2 >> W
+            ctr.max_col = max(ctr.max_col, max(T1), max(T2))
+        a2 = _norm_value(T1)
+        c2 = _norm_value(T2)
+        return a2, c2
+
+
+def limbs_loose(x, n):
+    """limbs with the top one unmasked (values up to ~b^n * 2)"""
+    out = [(x >> (W * i)) & MASK for i in range(n - 1)]
+    out.append(x >> (W * (n - 1)))
+    assert out[-1] < (1 << 32)
+    return out
+
+
+def _norm_value(T):
+    return sum(t << (W * i) for i, t in enumerate(T))
+
+
+def mont_digits_check(bits, trials, rng):
+    worst, amax, cmax = 0, 0, 0
+    for t in range(trials):
+        P = random_prime_like(bits // 2, rng)
+        D = MontDigits(P)
+        P2 = P * P
+        x = rng.randrange(P2)
+        state = D.to_form(x)
+        acc = x
+        for s in range(6):  # a chain, as the fixed-base loop runs it
+            y = rng.randrange(P2)
+            ctr = Counter()
+            state = D.mul(state, D.to_form(y), ctr)
+            acc = acc * y % P2
+            assert D.value(*state) == acc, "Montgomery-digit product wrong"
+            worst = max(worst, ctr.max_col)
+            amax = max(amax, state[0] / P)
+            cmax = max(cmax, (state[1] - D.R) / P)
+            assert state[1] < (1 << (W * D.k + 1)), "second digit outgrew its top limb"
+    return {"mont_digit_mads_per_product": ctr.mads, "mont_digit_product_ratio": ctr.mads / (2 * (2 * D.k) ** 2),
+            "mont_digit_max_column_log2": worst.bit_length(), "mont_digit_a_over_P": amax,
+            "mont_digit_c_minus_R_over_P": cmax, "mont_digit_chain_trials": trials}
+
+
 def random_prime_like(bits, rng):
     """an odd number with the top bit set (primality is irrelevant to the
     arithmetic being modelled)"""
@@ -177,6 +284,8 @@ def main():
     res["max_barrett_corrections"] = fix
     res["trials_bit_exact"] = args.trials
     assert worst_col < (1 << 64)
+    res.update(mont_digits_check(args.bits, max(4, args.trials // 10), rng))
+    assert res["mont_digit_max_column_log2"] <= 64
     print(json.dumps(res))
 
 

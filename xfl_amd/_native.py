@@ -322,7 +322,7 @@ class DeviceKey:
         self.private = bool(flags & 1)
         self.djn = bool(flags & 2)
         self.device = device
-        wb = (win_bits or int(os.environ.get("XHE_WIN_BITS", "0") or 16)) if self.private and self.djn else 0
+        wb = (win_bits or parse_win(os.environ.get("XHE_WIN_BITS", "0") or 16)) if self.private and self.djn else 0
         self.win_bits = wb & 0xFF  # the window w
         self.win_split = bool(wb & XHE_WIN_SPLIT)
 

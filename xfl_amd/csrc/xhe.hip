@@ -168,6 +168,9 @@ struct xhe_key {
   KeyDev kd{};
   std::vector<uint32_t> n_host;   // n words (for host-side checks)
   std::vector<uint32_t> n2_host;  // n^2 words (host inverse at the batch-inversion root)
+  int n_bits = 0;
+  int dneg = 0;  // smallest d with 1 << d >= min_value_for_negative (= n - n // 3): alignment gaps from
+                 // here on take _raw_mul's negative branch (paillier.py:79-86, 173-187)
 };
 
 namespace {
@@ -1101,6 +1104,31 @@ struct Stream {
   }
 };
 
+// After a ciphertext add whose alignment gap reaches key->dneg: the
+// reference's _decrease_exponent_to raises the operand of larger exponent to
+// the scalar 1 << d through _raw_mul, whose negative branch (1 << d >=
+// min_value_for_negative) gives c^(2^d - n) where the add kernel computed
+// c^(2^d) (paillier.py:79-86, 173-187). out *= x^-n with x = that operand on
+// those elements and 1 elsewhere: x^n by the per-element power, one batch
+// inversion, one product. Only reached when dmax >= dneg (gaps of ~bitlen(n)
+// exponent steps: precision=None values around 1e+-300).
+template <class Sh, class MN2>
+int mulmod_gap_fix(const xhe_key* k, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
+                   int64_t count, uint32_t* out, hipStream_t s) {
+  const size_t cb = (size_t)k->n2w * 4;
+  DevBuf x(count * cb, s), kx((size_t)count * k->nw * 4, s), z(count * cb, s), zi(count * cb, s), t(count * cb, s);
+  hipLaunchKernelGGL(k_gap_pick, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, k->kd, a, ea, b, eb, count,
+                     k->dneg, x.as<uint32_t>(), kx.as<uint32_t>());
+  HIPCHK(hipGetLastError());
+  powmod_impl<Sh, MN2>(k, x.as<uint32_t>(), kx.as<uint32_t>(), k->nw, k->n_bits, count, z.as<uint32_t>(), s);
+  const int rc = invert_impl<Sh, MN2>(k, z.as<uint32_t>(), count, zi.as<uint32_t>(), s);
+  if (rc != XHE_OK) return rc;
+  mulmod_impl<Sh, MN2>(k, out, nullptr, zi.as<uint32_t>(), nullptr, count, 0, t.as<uint32_t>(), nullptr, s);
+  HIPCHK(hipMemcpyAsync(out, t.p, count * cb, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // the DevBufs are freed on return
+  return XHE_OK;
+}
+
 // The stream-ordered allocator (hipMallocAsync, the entry points'
 // workspaces) returns freed memory to the device at each synchronisation by
 // default (release threshold 0), so every synchronised call would map its
@@ -1256,9 +1284,24 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
     for (size_t k = 0; k < parts.size(); ++k) dev.emplace_back(new DevBuf(parts[k], st(b).s));
   std::unique_ptr<PinnedSlots> pin;
   if (staged) pin.reset(new PinnedSlots(key->device, D, parts));
+  // Declared after `pin`, so destroyed before it: on every exit (a non-OK rc,
+  // a HIPCHK throw) the slot streams drain before the pinned ring goes back to
+  // the device's pool, where another caller may take it while this call's
+  // copies are still landing in it.
+  struct Drain {
+    std::vector<std::unique_ptr<Stream>>& s;
+    ~Drain() {
+      for (auto& x : s) (void)hipStreamSynchronize(x->s);
+    }
+  } drain{st_};
+  static const int64_t fail_chunk = [] {  // test hook: run() of this chunk fails (error-path tests)
+    const char* e = getenv("XHE_TEST_FAIL_CHUNK");
+    return e ? (int64_t)atoll(e) : (int64_t)-1;
+  }();
   auto dptr = [&](int b, int k) { return dev[(size_t)b * parts.size() + k]->p; };
   auto enqueue = [&](int64_t c) -> int {
     const int b = (int)(c % D);
+    if (c == fail_chunk) return fail(XHE_EINVAL, "host pipeline: injected failure (XHE_TEST_FAIL_CHUNK)");
     const int64_t off = c * chunk, n = std::min(chunk, count - off);
     hipStream_t s = st(b).s;
     const auto tin = std::chrono::steady_clock::now();
@@ -1367,8 +1410,9 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
       return fail(XHE_ENOTSUP, "xhe_key_create: key_bits must be 2048, 3072, 4096 or 8192");
     if ((p_words == nullptr) != (q_words == nullptr)) return fail(XHE_EINVAL, "xhe_key_create: need both p and q");
     if (win_bits == 0) {
-      const char* ev = getenv("XHE_WIN_BITS");
+      const char* ev = getenv("XHE_WIN_BITS");  // "23" or "23s" (split layout), as _native.parse_win
       win_bits = ev ? atoi(ev) : 16;
+      if (ev && win_bits > 0 && ev[strlen(ev) - 1] == 's') win_bits |= XHE_WIN_SPLIT;
     }
     const int wbase = win_bits & ~XHE_WIN_SPLIT;
     if (wbase < 2 || wbase > ((win_bits & XHE_WIN_SPLIT) ? 23 : 24))
@@ -1395,6 +1439,12 @@ int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint
     k->n_host.assign(n_words, n_words + k->nw);
     k->n2_host.assign(k->n2w, 0u);
     mul(n, n).to_words(k->n2_host.data(), k->n2w);
+    k->n_bits = (int)n.bits();
+    {
+      BigU third, rem;
+      divmod(n, BigU(3), &third, &rem);
+      k->dneg = (int)sub(sub(n, third), BigU(1)).bits();  // 2^d >= t  <=>  d >= bitlen(t - 1)
+    }
     BigU p, q, h;
     if (k->priv) {
       p = BigU::from_words(p_words, k->nw / 2);
@@ -1547,12 +1597,15 @@ int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev,
     DevGuard dg(key->device);
     const bool row = n2_row(count);
     hipStream_t hs = (hipStream_t)stream;
-    with_shape(key->K, [&](auto sh) {
+    return with_shape(key->K, [&](auto sh) -> int {
       using Sh = decltype(sh);
       if (row) mulmod_impl<Sh, typename Sh::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
       else mulmod_impl<Sh>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
+      if (ea_dev && eb_dev && dmax >= key->dneg)
+        return row ? mulmod_gap_fix<Sh, typename Sh::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, out_dev, hs)
+                   : mulmod_gap_fix<Sh, typename Sh::MN2>(key, a_dev, ea_dev, b_dev, eb_dev, count, out_dev, hs);
+      return XHE_OK;
     });
-    return XHE_OK;
   });
 }
 

@@ -1027,6 +1027,26 @@ __global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t
   if (eout && MN2::G::g() == 0) eout[e] = emin;
 }
 
+// Alignment across a gap d >= dneg (1 << d >= min_value_for_negative): the
+// reference's _decrease_exponent_to hands _raw_mul the scalar 1 << d, which
+// then takes the negative branch and yields c^(2^d - n) instead of c^(2^d)
+// (paillier.py:79-86, 173-187). For every element, x = the operand of larger
+// exponent when its gap is >= dneg, else 1, and k = n (the caller raises x to
+// k and inverts: out *= x^-n). One thread per element; rare path.
+__global__ void k_gap_pick(KeyDev key, const uint32_t* __restrict__ a, const int32_t* __restrict__ ea,
+                           const uint32_t* __restrict__ b, const int32_t* __restrict__ eb, int64_t count, int dneg,
+                           uint32_t* __restrict__ x, uint32_t* __restrict__ k) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const int64_t d = (int64_t)ea[e] - (int64_t)eb[e];
+  const bool big = (d < 0 ? -d : d) >= dneg;
+  const uint32_t* src = d > 0 ? a + (size_t)e * key.n2w : b + (size_t)e * key.n2w;
+  uint32_t* xo = x + (size_t)e * key.n2w;
+  for (int w = 0; w < key.n2w; ++w) xo[w] = big ? src[w] : (w == 0 ? 1u : 0u);
+  uint32_t* ko = k + (size_t)e * key.nw;
+  for (int w = 0; w < key.nw; ++w) ko[w] = key.n_words[w];
+}
+
 // out = c^k mod n^2 with a per-element exponent k (kw words, < 2^kbits).
 // Grid-stride; per-group workspace of 17 interleaved rows (4-bit window).
 template <class MN2>

@@ -225,8 +225,10 @@ class PaillierArray:
         return self._objects().tolist()
 
     def astype(self, dtype, copy=True):
+        """astype(object): the reference's np.ndarray[object] of
+        PaillierCiphertext (as np.asarray); other dtypes convert from it."""
         if np.dtype(dtype) == np.dtype(object):
-            return self.copy() if copy else self
+            return self._objects()
         return self._objects().astype(dtype)
 
     def _objects(self):
@@ -617,7 +619,8 @@ def _sum(x, axis=None, keepdims=False):
     order = perm.reshape(-1)
     w, e = _rows(x, order)
     seg = np.arange(nseg + 1, dtype=np.int64) * seglen
-    rw, re = ops.segment_sums_words(ctx, w, e, seg)
+    # numpy's add.reduce over an object array is a left fold in this order
+    rw, re = ops.segment_sums_words(ctx, w, e, seg, fold=True)
     if keepdims:
         out_shape = tuple(1 if d in axes else x.shape[d] for d in range(x.ndim))
     if not out_shape:

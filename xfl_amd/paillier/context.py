@@ -199,18 +199,28 @@ class PaillierContext(object):
     WIN_STEPS = ((0, 16), (8_000_000, 20), (64_000_000, 22))
     WIN_MARGIN = 32 << 30
 
-    def set_device_window(self, win_bits: Optional[int]):
-        """Pin the fixed-base window (None: back to the volume policy). Cached
-        device keys are rebuilt on next use."""
-        self._win_pinned = win_bits
+    def set_device_window(self, win_bits):
+        """Pin the fixed-base window: an int w, or '23s' / (23 | XHE_WIN_SPLIT)
+        for the split layout (None: back to the volume policy). Cached device
+        keys are rebuilt on next use."""
+        from .._native import parse_win
+        self._win_pinned = None if win_bits is None else parse_win(win_bits)
         self._dev = {}
 
     def _wanted_window(self):
-        pinned = getattr(self, "_win_pinned", None) or int(os.environ.get("XHE_WIN_BITS", "0") or 0)
+        """(window bits w, split layout) this context's tables should have."""
+        from .._native import XHE_WIN_SPLIT, parse_win
+        pinned = getattr(self, "_win_pinned", None) or parse_win(os.environ.get("XHE_WIN_BITS", "0") or 0)
         if pinned:
-            return pinned
+            return pinned & 0xFF, bool(pinned & XHE_WIN_SPLIT)
         vol = getattr(self, "_volume", 0)
-        return max(w for thr, w in self.WIN_STEPS if vol >= thr)
+        return max(w for thr, w in self.WIN_STEPS if vol >= thr), False
+
+    @staticmethod
+    def _key_fits(k, want):
+        """a built key serves a wanted (w, split) when its window is at least w
+        and its layout is the one asked for"""
+        return k.win_bits >= want[0] and getattr(k, "win_split", False) == want[1]
 
     def note_encrypt_volume(self, count: int):
         """Called by the batched encryptions: the policy's element counter."""
@@ -224,45 +234,59 @@ class PaillierContext(object):
             dev = self._dev = {}
         k = dev.get(device)
         fixed_base = self.__is_private and self.djn_on
-        if k is not None and (not fixed_base or k.win_bits >= self._wanted_window()):
+        if k is not None and (not fixed_base or self._key_fits(k, self._wanted_window())):
             return k
         with _KEY_LOCK:
             k = dev.get(device)
-            want = self._wanted_window() if fixed_base else 0
-            if k is not None and (not fixed_base or k.win_bits >= want):
+            want = self._wanted_window() if fixed_base else (0, False)
+            if k is not None and (not fixed_base or self._key_fits(k, want)):
                 return k
-            from .._native import DeviceKey, device_free_bytes, table_bytes
+            from .._native import XHE_WIN_SPLIT, DeviceKey, device_free_bytes, table_bytes
             bits = device_key_bits(self.__n)
             h = self.h_pow_n if self.djn_on else None
+            win, split = want
+            flag = XHE_WIN_SPLIT if split else 0
             if fixed_base:
-                have = table_bytes(bits, k.win_bits) if k is not None else 0
+                have = table_bytes(bits, k.win_bits | (XHE_WIN_SPLIT if k.win_split else 0)) if k is not None else 0
                 free = device_free_bytes(device)
-                while want > 16 and free is not None and table_bytes(bits, want) + self.WIN_MARGIN > free + have:
-                    want -= 2
-                if k is not None and k.win_bits >= want:
+                while win > 16 and free is not None and table_bytes(bits, win | flag) + self.WIN_MARGIN > free + have:
+                    win -= 2
+                if k is not None and self._key_fits(k, (win, split)):
                     return k
                 dev.pop(device, None)
                 k = None  # free the old tables before building the new ones
             if self.__is_private:
-                k = DeviceKey(bits, self.__n, self.__p, self.__q, h, device=device, win_bits=want)
+                k = DeviceKey(bits, self.__n, self.__p, self.__q, h, device=device, win_bits=win | flag if win else 0)
             else:
                 k = DeviceKey(bits, self.__n, None, None, h, device=device)
             dev[device] = k
         return k
 
     @staticmethod
+    def own_device():
+        """The GPU this process works on: $LOCAL_RANK (one rank per GPU, as
+        torch.distributed launches it) modulo the visible GPUs, else 0."""
+        from .._native import visible_devices
+        lr = os.environ.get("LOCAL_RANK", "").strip()
+        return int(lr) % visible_devices() if lr.isdigit() else 0
+
+    @staticmethod
     def shard_devices(num_cores: int = -1):
         """GPUs a batch is spread over (the reference spreads it over
         get_core_num(num_cores) processes, paillier.py:321-332,388-394):
-        $XHE_DEVICES (comma-separated ids, may repeat; "all") if set, else
-        num_cores == -1 -> every visible GPU, num_cores = k -> the first k."""
+        $XHE_DEVICES (comma-separated ids, may repeat; "all") if set; else
+        num_cores = k > 1 -> k GPUs starting at the process's own; else
+        (the default -1, or 1) the process's own GPU only. Fanning a default
+        call out over every GPU would give every rank of a multi-process job
+        a key - and, for a private DJN key, its fixed-base tables - on every
+        GPU of the node."""
         spec = os.environ.get("XHE_DEVICES", "").strip()
         if spec and spec != "all":
             return [int(d) for d in spec.split(",") if d.strip()]
         from .._native import visible_devices
         n = visible_devices()
-        if spec == "all" or num_cores is None or num_cores < 1:
-            k = n
-        else:
-            k = min(int(num_cores), n)
-        return list(range(max(1, k)))
+        if spec == "all":
+            return list(range(n))
+        own = PaillierContext.own_device()
+        k = 1 if num_cores is None or num_cores < 1 else min(int(num_cores), n)
+        return [(own + i) % n for i in range(k)]

@@ -239,11 +239,78 @@ def raw_mul_words(ctx, cw, kabs, neg, num_cores=-1):
     return out
 
 
-def segment_sums_words(ctx, cw, exps, seg_begin):
+def gap_threshold(ctx):
+    """Smallest alignment gap d with 1 << d >= min_value_for_negative: from
+    there on _decrease_exponent_to's scalar takes _raw_mul's negative branch,
+    c^(2^d - n) instead of c^(2^d) (paillier.py:79-86, 173-187)."""
+    return (int(ctx.min_value_for_negative) - 1).bit_length()
+
+
+def gap_power(ctx, D, bigs):
+    """The power a leaf of an addition tree ends up raised to when the
+    alignment shifts along its path sum to D and the ones in `bigs` took the
+    negative branch: exponents multiply along the path, each shift s
+    contributing 2^s, or 2^s - n when s >= gap_threshold."""
+    n = int(ctx.n)
+    E = 1 << (D - sum(bigs))
+    for s in bigs:
+        E *= (1 << s) - n
+    return E
+
+
+def fold_gap_powers(ctx, exps, seg_begin):
+    """Leaves of LEFT FOLDS (((x0 + x1) + x2) + ..., numpy's object-array
+    add.reduce and Python's sum) whose path crosses a negative-branch gap:
+    {leaf index: power} (gap_power). At step k the accumulator (exponent m =
+    min so far) meets x_k: x_k is aligned by e_k - m if larger, else every
+    leaf so far by m - e_k. Only segments whose exponent range reaches the
+    threshold are walked."""
+    dneg = gap_threshold(ctx)
+    seg = np.asarray(seg_begin, dtype=np.int64)
+    e = np.asarray(exps, dtype=np.int64).reshape(-1)
+    out = {}
+    if e.size == 0:
+        return out
+    lens = np.diff(seg)
+    nz = np.nonzero(lens > 0)[0]
+    rng = np.maximum.reduceat(e, seg[:-1][nz]) - np.minimum.reduceat(e, seg[:-1][nz])
+    for s in nz[rng >= dneg]:
+        lo, hi = int(seg[s]), int(seg[s + 1])
+        ev = [int(v) for v in e[lo:hi]]
+        m = ev[0]
+        own, drops = {}, []   # own[k]: x_k's own big shift; drops: (k, acc's big shift at step k)
+        for k in range(1, len(ev)):
+            if ev[k] - m >= dneg:
+                own[k] = ev[k] - m
+            elif m - ev[k] >= dneg:
+                drops.append((k, m - ev[k]))
+            m = min(m, ev[k])
+        for i in range(len(ev)):
+            bigs = ([own[i]] if i in own else []) + [d for k, d in drops if k > i]
+            if bigs:
+                out[lo + i] = gap_power(ctx, ev[i] - m, bigs)
+    return out
+
+
+def pow_signed_words(ctx, cw, powers):
+    """c_i^E_i mod n^2 for Python-int powers of either sign (a negative power
+    inverts first): the device's _raw_mul branches (paillier.py:173-187)."""
+    kabs = [abs(int(E)) for E in powers]
+    kw = max(1, (max(k.bit_length() for k in kabs) + 31) // 32)
+    return raw_mul_words(ctx, cw, nat.ints_to_words(kabs, kw), np.array([E < 0 for E in powers], dtype=bool))
+
+
+def segment_sums_words(ctx, cw, exps, seg_begin, gap_powers=None, fold=False):
     """Homomorphic sums of consecutive segments: segment s covers
     [seg_begin[s], seg_begin[s+1]); result exponent = min exponent of the
     segment (paillier.py:106-123 folded; order-free). An empty
-    segment gives 1 with exponent 0."""
+    segment gives 1 with exponent 0.
+
+    Past the negative-branch gap (gap_threshold) the reference's bits depend on
+    the addition tree: gap_powers {leaf: power} (gap_power) gives those
+    leaves' final powers, or fold=True derives them for left folds of each
+    segment in input order (fold_gap_powers); such leaves are raised to their
+    power first and enter the product unaligned."""
     seg = np.ascontiguousarray(seg_begin, dtype=np.int64)
     nseg = seg.shape[0] - 1
     cw = _u32(cw)
@@ -255,14 +322,30 @@ def segment_sums_words(ctx, cw, exps, seg_begin):
     if n:
         emin[nz] = np.minimum.reduceat(e, seg[:-1][nz])
     d = (e - np.repeat(emin, lens)).astype(np.int32)
+    if fold and n and gap_powers is None:
+        gap_powers = fold_gap_powers(ctx, e, seg)
+    if gap_powers:
+        idx = np.fromiter(gap_powers.keys(), dtype=np.int64, count=len(gap_powers))
+        cw = cw.copy()
+        cw[idx] = pow_signed_words(ctx, cw[idx], [gap_powers[int(i)] for i in idx])
+        d[idx] = 0
+    return segprod_words(ctx, cw, d, seg), emin.astype(np.int32)
+
+
+def segprod_words(ctx, cw, d, seg):
+    """out[s] = prod_{i in segment s} c_i^(2^d_i) mod n^2: one xhe_segprod
+    call (int32 d >= 0, int64 seg offsets)."""
+    n = cw.shape[0]
+    nseg = seg.shape[0] - 1
     dmax = int(d.max()) if n else 0
     n2w = n2w_of(ctx)
     src = cw if n else np.zeros((1, n2w), dtype=np.uint32)
+    d = _i32(d)
     out = np.empty((nseg, n2w), dtype=np.uint32)
     dk = ctx.device_key()
     nat.check(nat.lib().xhe_segprod_host(dk.handle, _vp(src), _vp(d) if dmax else None, dmax, n, _vp(seg), nseg,
                                          _vp(out)), "segprod")
-    return out, emin.astype(np.int32)
+    return out
 
 
 def multiexp_words(ctx, bw, idx, kw_, kbits, win_bits=0):
@@ -326,17 +409,15 @@ def powmod(ctx, raws, ks, invert_first=False):
 
 
 def raw_mul(ctx, raws, ks):
-    """_raw_mul for encoded k in [0, n): inv(c)^(n-k) when k >=
-    min_value_for_negative, else c^k."""
+    """_raw_mul (paillier.py:156-187) for k >= 0: c^(k - n) when k >=
+    min_value_for_negative (inv(c)^(n - k) for k < n; _decrease_exponent_to's
+    1 << d may exceed n, and then the power k - n is positive), else c^k."""
     n = len(raws)
     if n == 0:
         return []
     thr = ctx.min_value_for_negative
-    neg = np.array([k >= thr for k in ks], dtype=bool)
-    kabs = [ctx.n - k if g else k for k, g in zip(ks, neg)]
-    kbits = max(1, max(int(k).bit_length() for k in kabs))
-    out = raw_mul_words(ctx, nat.ints_to_words(raws, n2w_of(ctx)), nat.ints_to_words(kabs, (kbits + 31) // 32), neg)
-    return nat.words_to_ints(out)
+    return nat.words_to_ints(pow_signed_words(ctx, nat.ints_to_words(raws, n2w_of(ctx)),
+                                              [int(k) - ctx.n if k >= thr else int(k) for k in ks]))
 
 
 def obfuscate(ctx, raws):
@@ -345,10 +426,10 @@ def obfuscate(ctx, raws):
     return nat.words_to_ints(obfuscate_words(ctx, nat.ints_to_words(raws, n2w_of(ctx))))
 
 
-def segment_sums(ctx, raws, exps, seg_begin):
+def segment_sums(ctx, raws, exps, seg_begin, gap_powers=None):
     n2w = n2w_of(ctx)
     cw = nat.ints_to_words(raws, n2w) if len(raws) else np.zeros((0, n2w), dtype=np.uint32)
-    out, emin = segment_sums_words(ctx, cw, exps, seg_begin)
+    out, emin = segment_sums_words(ctx, cw, exps, seg_begin, gap_powers=gap_powers)
     return nat.words_to_ints(out), emin
 
 

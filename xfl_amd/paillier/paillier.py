@@ -164,17 +164,23 @@ def materialize(cts):
             by_ctx.setdefault(id(c.context), []).append(c)
     for group in by_ctx.values():
         raws, exps, seg = [], [], [0]
+        gaps = {}  # leaves whose path crosses a negative-branch alignment (ops.gap_power)
+        dneg = ops.gap_threshold(group[0].context)
         for root in group:
-            stack = [root]
+            stack = [(root, ())]
             while stack:  # iterative: addition chains can be 10^5 deep
-                node = stack.pop()
+                node, bigs = stack.pop()
                 if node._is_deferred():
-                    stack.extend(node._parts)
+                    for part in node._parts:
+                        s = part.exponent - node.exponent  # the shift _add_encrypted aligns `part` by
+                        stack.append((part, bigs + (s,) if s >= dneg else bigs))
                 else:
+                    if bigs:
+                        gaps[len(raws)] = ops.gap_power(node.context, node.exponent - root.exponent, bigs)
                     raws.append(node.raw_ciphertext)
                     exps.append(node.exponent)
             seg.append(len(raws))
-        r, e = ops.segment_sums(group[0].context, raws, exps, seg)
+        r, e = ops.segment_sums(group[0].context, raws, exps, seg, gap_powers=gaps)
         for root, rv, ev in zip(group, r, e):
             assert int(ev) == root.exponent
             root._set_raw(rv)
