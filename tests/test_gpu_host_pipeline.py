@@ -146,3 +146,53 @@ def test_decrypt_host_chunked(env):
     f64b = np.empty(n)
     nat.check(L.xhe_decrypt_decode_host(dk.handle, vp(c), vp(ex), n, vp(f64b), vp(f32), vp(st), None), "dd2")
     assert np.array_equal(f64b[ok].view(np.uint64), f64[ok].view(np.uint64))
+
+
+_FAIL_SCRIPT = r"""
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, {root!r})
+import torch
+torch.cuda.init()
+from tests.conftest import FIXTURES, hx, load_fixture
+from tests.test_gpu_parity import _dkey
+from xfl_amd import _native as nat
+L = nat.lib()
+dk = _dkey(load_fixture(FIXTURES[0]))
+vp = lambda a: ctypes.c_void_p(a.ctypes.data)
+n = 5 * (1 << 17) + 17            # 6 chunks of xhe_encrypt_host (128 k), staged through the pinned ring
+rng = np.random.default_rng(3)
+m = rng.integers(0, 1 << 32, (n, dk.nw), dtype=np.uint64).astype(np.uint32)
+m[:, dk.nw - 1:] = 0
+r = rng.integers(0, 1 << 32, (n, dk.rand_words), dtype=np.uint64).astype(np.uint32)
+r[:, 0] |= 1
+out = np.zeros((n, dk.n2w), np.uint32)
+rc = L.xhe_encrypt_host(dk.handle, vp(m), vp(r), n, vp(out))
+assert rc == nat.XHE_EINVAL and b"injected" in L.xhe_last_error(), (rc, L.xhe_last_error())
+# the ring is free again and holds no stale copies: a full call in the same
+# process equals the device-resident result
+out2 = np.zeros((n, dk.n2w), np.uint32)
+nat.check(L.xhe_encrypt_host(dk.handle, vp(m), vp(r), n, vp(out2)), "encrypt_host")
+md, rd = torch.from_numpy(m.view(np.int32)).cuda(), torch.from_numpy(r.view(np.int32)).cuda()
+c = torch.empty((n, dk.n2w), dtype=torch.int32, device="cuda")
+nat.check(L.xhe_encrypt(dk.handle, md.data_ptr(), rd.data_ptr(), n, c.data_ptr(), torch.cuda.current_stream().cuda_stream))
+torch.cuda.synchronize()
+assert np.array_equal(out2, c.cpu().numpy().view(np.uint32))
+print("ok")
+"""
+
+
+def test_failing_chunk_leaves_pipeline_usable():
+    """A run() that fails in the middle of a multi-chunk call (the
+    $XHE_TEST_FAIL_CHUNK hook, chunk 3 of 6) returns its error after the slot
+    streams have drained (the pinned ring is released last); the next call in
+    the same process is bit-exact."""
+    import os
+    import subprocess
+    import sys
+
+    from tests.conftest import ROOT
+    env_ = dict(os.environ, XHE_TEST_FAIL_CHUNK="3")
+    r = subprocess.run([sys.executable, "-c", _FAIL_SCRIPT.format(root=ROOT)], env=env_, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

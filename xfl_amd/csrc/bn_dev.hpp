@@ -52,6 +52,9 @@ namespace xhe {
 #ifndef XHE_SQ_ACC
 #define XHE_SQ_ACC 2  // partial sums per column of Mont::sqr's product scan
 #endif
+#ifndef XHE_PMD
+#define XHE_PMD 1  // 2048-bit DJN tables as Montgomery digits, encrypted by k_djn_pmd (pdigit_dev.hpp)
+#endif
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif

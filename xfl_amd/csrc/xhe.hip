@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <memory>
 #include <mutex>
+#include <atomic>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -317,6 +318,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t nR2_p2 = 0, nR2_q2 = 0, q2invR = 0, q2_lim = 0, p2x4 = 0, hM_p2 = 0, hM_q2 = 0;
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
+    size_t topc_p = 0, topc_q = 0;
   } o;
   int pm1_bits = 0, qm1_bits = 0, ep_bits = 0, eq_bits = 0;
   if (k->priv) {
@@ -392,6 +394,19 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o.hqR = bl.put_limbs(mulmod(hq, Rq, Q), s1);
     o.qinvpR = bl.put_limbs(mulmod(modinv(Q, P), Rp, P), s1);  // context.py:43
     o.q_lim = bl.put_limbs(Q, s1);
+#if XHE_PMD && XHE_LDS_ROWS
+    if (k->djn && K == 2048) {
+      // Montgomery-digit encryption (k_djn_pmd): MASK + E_i, E = (1 - R) mod P,
+      // R = 2^(28*37) (= the mod-p shape's R, so R mod P is kd.p.R1)
+      auto topc = [&](const BigU& X) {
+        std::vector<uint32_t> v = submod(BigU(1), mod(T, X), X).to_limbs(28, 37);
+        for (auto& x : v) x += (1u << 28) - 1u;
+        return bl.put(v);
+      };
+      o.topc_p = topc(P);
+      o.topc_q = topc(Q);
+    }
+#endif
     o.p2x = bl.put_limbs(shl(P, 1), s1);
     o.p_lim = bl.put_limbs(P, s1);
     // non-DJN private obfuscation exponents ep = n mod phi(p^2) (context.py:51-52)
@@ -480,6 +495,22 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
         using Sh = decltype(sh);
         build_tables_sync<typename Sh::MP2, Sh::RW>(k, mds, hms, tabs, 2);
       });
+#if XHE_PMD && XHE_LDS_ROWS
+      if (K == 2048) {
+        // rows as Montgomery digits (e, f) for k_djn_pmd
+        kd.pmd = 1;
+        kd.topc_p = B + o.topc_p;
+        kd.topc_q = B + o.topc_q;
+        const int64_t trows = (int64_t)(kd.nwin + kd.nhi) << kd.win;
+        const ModDev mp[2] = {kd.p, kd.q};
+        for (int i = 0; i < 2; ++i) {
+          hipLaunchKernelGGL((k_tab_to_pmd<37, 64>), dim3((unsigned)((trows + 255) / 256)), dim3(256), 0, nullptr,
+                             mp[i].N, mp[i].n0inv, mp[i].R1, tabs[i], trows, (int64_t)kd.tab_rs);
+          HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipDeviceSynchronize());
+      }
+#endif
     }
   }
   if (!k->priv && k->djn) {
@@ -624,6 +655,20 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
+#if XHE_PMD && XHE_LDS_ROWS
+    if constexpr (Sh::K == 2048) {
+      if (k->kd.pmd) {
+        ProfScope ps("k_djn_pow", s);
+        const dim3 grid((unsigned)((n + 127) / 128), 2);
+        hipLaunchKernelGGL((k_djn_pmd<MP2, 37, Sh::RW>), grid, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N,
+                           k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
+                           k->rand_words, n, ws);
+        HIPCHK(hipGetLastError());
+        crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
+        continue;
+      }
+    }
+#endif
     if (enc_row(n)) {
       // small batch: one 16-lane DPP row per residue (latency-bound regime)
       using MX = typename Sh::MP2X;
@@ -1301,7 +1346,9 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
   auto dptr = [&](int b, int k) { return dev[(size_t)b * parts.size() + k]->p; };
   auto enqueue = [&](int64_t c) -> int {
     const int b = (int)(c % D);
-    if (c == fail_chunk) return fail(XHE_EINVAL, "host pipeline: injected failure (XHE_TEST_FAIL_CHUNK)");
+    static std::atomic<bool> fired{false};  // the hook fails one call per process
+    if (c == fail_chunk && !fired.exchange(true))
+      return fail(XHE_EINVAL, "host pipeline: injected failure (XHE_TEST_FAIL_CHUNK)");
     const int64_t off = c * chunk, n = std::min(chunk, count - off);
     hipStream_t s = st(b).s;
     const auto tin = std::chrono::steady_clock::now();

@@ -9,6 +9,7 @@
 //   decode            encoder.py:56-64, paillier.py:396-403
 #pragma once
 #include "bn_dev.hpp"
+#include "pdigit_dev.hpp"
 
 namespace xhe {
 
@@ -71,6 +72,10 @@ struct KeyDev {
   const uint32_t* q_lim;      // q (MP limbs)
   const uint32_t* p2x_lim;    // 2 p (MP limbs)
   const uint32_t* p_lim;      // p (MP limbs)
+  // ---- Montgomery-digit DJN encryption (k_djn_pmd, 2048-bit keys): the
+  // tables hold digit pairs (pmd = 1); MASK + ((1 - R) mod P) limbs per prime
+  int pmd;
+  const uint32_t *topc_p, *topc_q;
 };
 
 // ============================================================== encode
@@ -580,6 +585,129 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
                      prime, img, img + (threadIdx.x & 63) * 4, ws);
 }
 
+#endif
+
+#if XHE_PMD && XHE_LDS_ROWS
+// ---------------------------------------------------------------------------
+// DJN encryption in Montgomery digits (pdigit_dev.hpp PMD; 2048-bit keys,
+// K = 37 limbs of P): c_P = (1 + n m) h^a mod P^2 as k_djn_pow_lds computes
+// it, with the table products in digit form. The tables hold each row as its
+// digits (e, f) < P (k_tab_to_pmd), packed 32 + 32 words. Per prime and
+// element: the first window's row is the start value; each further window's
+// row is LDS-DMA'd into the wave's image, unpacked into interleaved limb
+// pairs, and multiplied in (nwin - 1 digit products, 5 K^2 mads each); the
+// result goes back to the 74-limb Montgomery form (R a + P c = h^a R^2 mod
+// P^2, to_mont2) for the two Montgomery products that bring in (1 + n m) and
+// leave Montgomery form, exactly as in djn_prime_lds. Output rows as
+// k_djn_pow_lds (MP2 limbs, [prime][2 S4][count]) for k_crt_enc_w.
+template <class MP2, int KP, int RW>
+__global__ void __launch_bounds__(128, 2) k_djn_pmd(KeyDev key, const uint32_t* __restrict__ Pp,
+                                                    const uint32_t* __restrict__ Pq, const uint32_t* __restrict__ Np2,
+                                                    const uint32_t* __restrict__ Nq2,
+                                                    const uint32_t* __restrict__ m_words,
+                                                    const uint32_t* __restrict__ a_words, int aw, int64_t count,
+                                                    uint32_t* __restrict__ ws) {
+  static_assert(MP2::TPI == 1 && MP2::S == 2 * KP && MP2::W == 28, "digits of the one-lane P^2 shape");
+  using D = PMD<KP>;
+  constexpr int NQ = D::NQ > MP2::S4 / 4 ? D::NQ : MP2::S4 / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][NQ * 256];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[(KP + 3) & ~3];
+  const int prime = blockIdx.y;
+  const uint32_t* tc = prime ? key.topc_q : key.topc_p;
+  if (threadIdx.x < KP) topc[threadIdx.x] = tc[threadIdx.x];
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
+  uint32_t* slot = img + (threadIdx.x & 63) * 4;
+  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  D M;
+  M.init(prime ? Pq : Pp, prime ? key.q.n0inv : key.p.n0inv);
+  auto stage = [&](int w) XHE_INL {
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    const uint32_t* row = tab + (size_t)(row0 + d) * key.tab_rs;
+#pragma unroll
+    for (int k = 0; k < RW / 4; ++k)
+      __builtin_amdgcn_global_load_lds((xhe_glb_void*)(row + 4 * k), (xhe_lds_void*)(img + k * 256), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unpack_pairs_lds<KP, RW>(slot);
+  };
+  uint32_t a[KP], c[KP];
+  stage(0);
+#pragma unroll
+  for (int q = 0; q < D::NQ; ++q) {
+    const uint4 v = *reinterpret_cast<const uint4*>(slot + q * 256);
+    if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+    if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+  }
+  for (int w = 1; w < key.nwin; ++w) {
+    stage(w);
+    M.mul(a, c, slot, topc);
+  }
+  {
+    uint32_t x[2 * KP];
+    M.to_mont2(a, c, x);  // h^a R^2 mod P^2, unreduced (< 2^13 P^2)
+#pragma unroll
+    for (int q = 0; q < MP2::S4 / 4; ++q)
+      *reinterpret_cast<uint4*>(slot + q * 256) =
+          make_uint4(4 * q < 2 * KP ? x[4 * q] : 0u, 4 * q + 1 < 2 * KP ? x[4 * q + 1] : 0u,
+                     4 * q + 2 < 2 * KP ? x[4 * q + 2] : 0u, 4 * q + 3 < 2 * KP ? x[4 * q + 3] : 0u);
+  }
+  MP2 N;
+  N.init(prime ? Nq2 : Np2, prime ? key.q2.n0inv : key.p2.n0inv);
+  uint32_t b[MP2::L];
+  N.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  N.mul(b, ARow{prime ? key.nR_q2 : key.nR_p2});  // n m mod P^2 (< 2 P^2), plain
+  b[0] += 1u;                                     // 1 + n m
+  N.mul(b, ALdsQ{slot});                          // (1 + n m) h^a mod P^2
+  N.reduce_once(b);
+  N.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+}
+
+// Rewrite packed fixed-base table rows X = x R^2 mod P^2 (the 74-limb
+// Montgomery form k_tab_combine writes, RW words) as their Montgomery digits
+// (e, f) < P, RW/2 words each (pdigit_dev.hpp pmd_from_mont2). One thread per
+// row, in place; once per key after the table build.
+template <int KP, int RW>
+__global__ void __launch_bounds__(256, 2) k_tab_to_pmd(const uint32_t* __restrict__ P, uint32_t n0inv,
+                                                       const uint32_t* __restrict__ RmodP, uint32_t* __restrict__ tab,
+                                                       int64_t rows, int64_t rs) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  uint32_t* row = tab + (size_t)r * rs;
+  uint32_t w[RW];
+#pragma unroll
+  for (int q = 0; q < RW / 4; ++q) {
+    const uint4 v = reinterpret_cast<const uint4*>(row)[q];
+    w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
+  }
+  uint32_t X[2 * KP];
+#pragma unroll
+  for (int l = 0; l < 2 * KP; ++l) {
+    const int bit = 28 * l, k = bit >> 5, sh = bit & 31;
+    const uint32_t lo = k < RW ? w[k] : 0u, hi = k + 1 < RW ? w[k + 1] : 0u;
+    X[l] = __builtin_amdgcn_alignbit(hi, lo, sh) & ((1u << 28) - 1u);
+  }
+  PMD<KP> M;
+  M.init(P, n0inv);
+  uint32_t e[KP], f[KP];
+  pmd_from_mont2<KP>(M, X, RmodP, e, f);
+  auto word = [&](const uint32_t (&l)[KP], int k) -> uint32_t {
+    const int bit = 32 * k, j = bit / 28, sh = bit - 28 * j;
+    uint64_t v = (uint64_t)l[j] >> sh;
+    if (j + 1 < KP) v |= (uint64_t)l[j + 1] << (28 - sh);
+    if (j + 2 < KP) v |= (uint64_t)l[j + 2] << (56 - sh);
+    return (uint32_t)v;
+  };
+#pragma unroll
+  for (int q = 0; q < RW / 8; ++q) {
+    reinterpret_cast<uint4*>(row)[q] = make_uint4(word(e, 4 * q), word(e, 4 * q + 1), word(e, 4 * q + 2), word(e, 4 * q + 3));
+    reinterpret_cast<uint4*>(row)[RW / 8 + q] =
+        make_uint4(word(f, 4 * q), word(f, 4 * q + 1), word(f, 4 * q + 2), word(f, 4 * q + 3));
+  }
+}
 #endif
 
 // c = c_q + q^2 ((c_p + 4p^2 - c_q) (q^2)^-1 mod p^2) for element e (utils.py:38-43)
