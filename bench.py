@@ -119,15 +119,17 @@ def pmc_traffic(win_bits, n):
     this configuration; else None. Counters cannot be read inside this run
     (rocprofv3 --pmc is its own pass)."""
     from xfl_amd._native import win_spec
-    path = os.path.join(ROOT, "profiles", "r2", "k_djn_pow_pmc.json")
-    try:
-        with open(path) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
-        return None, None
-    return rec["traffic_bytes"], os.path.relpath(path, ROOT)
+    for rnd in ("r3", "r2"):  # the newest round's passes (the kernel changed between rounds)
+        path = os.path.join(ROOT, "profiles", rnd, "k_djn_pow_pmc.json")
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
+            return None, None
+        return rec["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def _timed(fn, reps=3):

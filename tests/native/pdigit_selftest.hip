@@ -57,6 +57,24 @@ __global__ void __launch_bounds__(128, 2) k_check(const uint32_t* P, uint32_t n0
       state[(size_t)e * 2 * K + j] = a[j];
       state[(size_t)e * 2 * K + K + j] = c[j];
     }
+  } else if (mode == 3) {  // state <- state^2 (the state parked in the slot, as the decrypt does)
+    uint32_t a[K], c[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      a[j] = state[(size_t)e * 2 * K + j];
+      c[j] = state[(size_t)e * 2 * K + K + j];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      *reinterpret_cast<uint4*>(slot + q * 256) =
+          make_uint4(2 * q < K ? a[2 * q] : 0u, 2 * q < K ? c[2 * q] : 0u, 2 * q + 1 < K ? a[2 * q + 1] : 0u,
+                     2 * q + 1 < K ? c[2 * q + 1] : 0u);
+    M.sqr(a, c, slot, topc);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      state[(size_t)e * 2 * K + j] = a[j];
+      state[(size_t)e * 2 * K + K + j] = c[j];
+    }
   } else if (mode == 1) {
     uint32_t a[K], c[K], x[2 * K];
 #pragma unroll
@@ -260,6 +278,26 @@ int main() {
       }
     }
     printf("{\"check\": \"mul\", \"bad\": %d, \"out_of_range\": %d, \"of\": %d}\n", bad, range, count * chain);
+    rc |= bad != 0 || range != 0;
+    // squaring chains continue from the product chains' states
+    bad = range = 0;
+    for (int t = 0; t < chain; ++t) {
+      for (int i = 0; i < count; ++i) acc[i] = mulmod(acc[i], acc[i], P2);
+      hipLaunchKernelGGL(k_check, dim3(count / 128), dim3(128), 0, 0, dP, n0, dtopc, dRp, drows, dstate, dout, count,
+                         3);
+      if (hipMemcpy(hstate.data(), dstate, hstate.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        printf("{\"error\": \"hip\"}\n");
+        return 1;
+      }
+      const BigU cmax = add(R, mul(P, BigU(8)));
+      const BigU amax = mul(P, BigU(2));
+      for (int i = 0; i < count; ++i) {
+        BigU a = from_limbs(&hstate[(size_t)i * 2 * K], K), c = from_limbs(&hstate[(size_t)i * 2 * K + K], K);
+        if (cmp(value(a, c), acc[i]) != 0 && ++bad < 4) printf("  sqr chain %d elem %d: wrong value\n", t, i);
+        if (cmp(a, amax) >= 0 || cmp(c, cmax) >= 0) ++range;
+      }
+    }
+    printf("{\"check\": \"sqr\", \"bad\": %d, \"out_of_range\": %d, \"of\": %d}\n", bad, range, count * chain);
     rc |= bad != 0 || range != 0;
   }
   // 2. to_mont2 of the final states: R a + P c (74 limbs, exact integer)

@@ -99,11 +99,35 @@ struct PMD {
         : "vcc");
   }
 
+  // squaring form of blk2: T2[j-1+k] = T2[j+k] + e2 c[j+k] + m P[j+k] (e2 = 2 a_i)
+  XHE_DEV void blk2s(uint64_t (&T)[K], const uint32_t (&c)[K], uint32_t e2, uint32_t m, int j) const {
+    asm("v_mad_u64_u32 %0, vcc, %7, %9, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %7, %10, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %7, %11, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %7, %12, %4\n\t"
+        "v_mad_u64_u32 %4, vcc, %7, %13, %5\n\t"
+        "v_mad_u64_u32 %5, vcc, %7, %14, %6\n\t"
+        "v_mad_u64_u32 %0, vcc, %8, %15, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %8, %16, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %8, %17, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %8, %18, %3\n\t"
+        "v_mad_u64_u32 %4, vcc, %8, %19, %4\n\t"
+        "v_mad_u64_u32 %5, vcc, %8, %20, %5"
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4])
+        : "v"(T[j + 5]), "v"(e2), "v"(m), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]), "v"(c[j + 3]), "v"(c[j + 4]),
+          "v"(c[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]), "s"(p[j + 4]), "s"(p[j + 5])
+        : "vcc");
+  }
+
   // One step of the two interleaved reductions on row limbs (e, f). Entry:
   // x1 = T1[0] + e a[0], x2 = T2[0] + e c[0] + f a[0] and their digits m1, m2;
   // the next step's (en, fn) values are formed under this step's mads (each
   // link of that dependent chain after its own block pair, as Mont::step1).
   // topc = MASK + E_i.
+  // SQ: the squaring step - (e, f) = (a_i, c_i) of the state itself, and
+  // T2 takes (2 a_i) c instead of a_i c + c_i a (the same sum, 2 a c: K mads
+  // fewer per step; 2 a_i < 2^29 keeps every accumulator below 2^63).
+  template <bool SQ = false>
   XHE_DEV void step(uint64_t (&T1)[K], uint64_t (&T2)[K], const uint32_t (&a)[K], const uint32_t (&c)[K],
                     uint32_t e, uint32_t f, uint32_t en, uint32_t fn, uint32_t& m1, uint32_t& m2, uint64_t& x1,
                     uint64_t& x2, uint32_t topc) const {
@@ -115,14 +139,16 @@ struct PMD {
     for (int b = 0; b < (K - 1) / BL; ++b) {
       const int j = 1 + BL * b;
       blk1(T1, a, e, m1, j);
-      blk2(T2, c, a, e, f, m2, j);
+      if constexpr (SQ) blk2s(T2, c, e << 1, m2, j);
+      else blk2(T2, c, a, e, f, m2, j);
       if (b == 0) {
         T1[0] += x1 >> W;
         T2[0] += x2 >> W;
         asm volatile("" : "+v"(T1[0]), "+v"(T2[0]));
       } else if (b == 1) {
         x1n = mad64(en, a[0], T1[0]);
-        x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
+        if constexpr (SQ) x2n = mad64(en << 1, c[0], T2[0]);
+        else x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
         asm volatile("" : "+v"(x1n), "+v"(x2n));
       } else if (b == 2) {
         t1 = (uint32_t)x1n * n0inv;
@@ -147,24 +173,38 @@ struct PMD {
   // slot of a quad-major LDS image (quad q = e_2q, f_2q, e_2q+1, f_2q+1 at
   // slot[q * 256]); topc: K words MASK + E_i (LDS, shared by the block).
   XHE_DEV void mul(uint32_t (&a)[K], uint32_t (&c)[K], const uint32_t* slot, const uint32_t* topc) const {
+    run<false>(a, c, slot, topc);
+  }
+  // (a, c) <- (a, c)^2: the state parked in the slot (same layout) as the
+  // streamed operand; 4 K^2 mads (squaring steps)
+  XHE_DEV void sqr(uint32_t (&a)[K], uint32_t (&c)[K], const uint32_t* slot, const uint32_t* topc) const {
+    run<true>(a, c, slot, topc);
+  }
+  template <bool SQ>
+  XHE_DEV void run(uint32_t (&a)[K], uint32_t (&c)[K], const uint32_t* slot, const uint32_t* topc) const {
     uint64_t T1[K], T2[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) T1[j] = T2[j] = 0;
-    uint4 cur = *reinterpret_cast<const uint4*>(slot);
-    uint64_t x1 = mad64(cur.x, a[0], 0ull);
-    uint64_t x2 = mad64(cur.y, a[0], mad64(cur.x, c[0], 0ull));
+    // one (e_i, f_i) pair in flight ahead of the step that consumes it (a
+    // ds_read_b64 at the start of the step before): 4 row registers live
+    // instead of two whole quads
+    uint2 p0 = *reinterpret_cast<const uint2*>(slot);
+    uint64_t x1 = mad64(p0.x, a[0], 0ull);
+    uint64_t x2 = SQ ? mad64(p0.x << 1, c[0], 0ull) : mad64(p0.y, a[0], mad64(p0.x, c[0], 0ull));
     uint32_t m1 = ((uint32_t)x1 * n0inv) & MASK, m2 = ((uint32_t)x2 * n0inv) & MASK;
     for (int q = 0; q < K / 2; ++q) {
-      const uint4 nxt = *reinterpret_cast<const uint4*>(slot + (q + 1) * 256);
+      const uint32_t* sq = slot + q * 256;
       const uint2 tc = *reinterpret_cast<const uint2*>(topc + 2 * q);
+      const uint2 p1 = *reinterpret_cast<const uint2*>(sq + 2);
       __builtin_amdgcn_sched_barrier(0);
-      step(T1, T2, a, c, cur.x, cur.y, cur.z, cur.w, m1, m2, x1, x2, tc.x);
+      step<SQ>(T1, T2, a, c, p0.x, p0.y, p1.x, p1.y, m1, m2, x1, x2, tc.x);
       __builtin_amdgcn_sched_barrier(0);
-      step(T1, T2, a, c, cur.z, cur.w, nxt.x, nxt.y, m1, m2, x1, x2, tc.y);
+      p0 = *reinterpret_cast<const uint2*>(sq + 256);
       __builtin_amdgcn_sched_barrier(0);
-      cur = nxt;
+      step<SQ>(T1, T2, a, c, p1.x, p1.y, p0.x, p0.y, m1, m2, x1, x2, tc.y);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (K & 1) step(T1, T2, a, c, cur.x, cur.y, 0u, 0u, m1, m2, x1, x2, topc[K - 1]);
+    if constexpr (K & 1) step<SQ>(T1, T2, a, c, p0.x, p0.y, 0u, 0u, m1, m2, x1, x2, topc[K - 1]);
     normalize(T1, a);
     normalize(T2, c);
   }
@@ -224,6 +264,7 @@ XHE_DEV void pmd_redc_wide(const PMD<K>& M, uint64_t (&T)[2 * K], uint32_t (&t)[
     cy = x >> 28;
 #pragma unroll
     for (int j = 1; j < K; ++j) T[i + j] = mad64s(mi, M.p[j], T[i + j]);
+    __builtin_amdgcn_sched_barrier(0);  // one row at a time (rows interleaved by the scheduler spill)
   }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -246,52 +287,81 @@ XHE_DEV uint32_t pmd_sub(uint32_t (&r)[K], const uint32_t (&s)[K]) {
   return br ? 1u : 0u;
 }
 
+// r <- r - P if r >= P (r < 2^(28K)); returns whether it subtracted. Two
+// passes (the borrow of r - P, then a masked subtraction) instead of a copy
+// and a select: no second K-limb temporary.
+template <int K>
+XHE_DEV bool pmd_csub(const PMD<K>& M, uint32_t (&r)[K]) {
+  int64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) br = ((int64_t)r[j] - (int64_t)M.p[j] + br) >> 28;
+  const bool ge = br == 0;
+  br = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int64_t v = (int64_t)r[j] - (int64_t)(ge ? M.p[j] : 0u) + br;
+    r[j] = (uint32_t)v & ((1u << 28) - 1u);
+    br = v >> 28;
+  }
+  return ge;
+}
+
+// m mod P for 0 <= m < 2^(28K) (< 2^13 P at K = 37), in place: one
+// quotient limb q from 32-bit tops (m >> (28K - 32) over (P >> (28K - 32))
+// + 1; P >= 2^(28K - 13), so the estimate is at most 3 below floor(m / P)),
+// then m - q P and three conditional subtractions of P.
+template <int K>
+XHE_DEV void pmd_mod_small(const PMD<K>& M, uint32_t (&m)[K]) {
+  constexpr uint32_t MASK = PMD<K>::MASK;
+  const uint32_t mt = (m[K - 1] << 4) | (m[K - 2] >> 24);      // bits [28K - 32, 28K)
+  const uint32_t pt = (M.p[K - 1] << 4) | (M.p[K - 2] >> 24);  // >= 2^19
+  const uint32_t q = mt / (pt + 1u);
+  uint64_t cy = 0;
+  int64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint64_t qp = (uint64_t)q * M.p[j] + cy;
+    cy = qp >> 28;
+    const int64_t v = (int64_t)m[j] - (int64_t)(qp & MASK) + br;
+    m[j] = (uint32_t)v & MASK;
+    br = v >> 28;
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t) pmd_csub<K>(M, m);
+}
+
 // Table-row conversion: a reduced residue X = x R^2 mod P^2 (< P^2, 2K limbs:
 // the 74-limb Montgomery form the table kernels produce) into its Montgomery
 // digits (e, f), both in [0, P). REDC gives X = R t - m P with t < 2P, m <
-// R; then e = t mod P and f = (-m + [t >= P] R) mod P, where m mod P is one
-// more REDC: MontMul(m, R mod P) = m (mod P).
+// R; then e = t mod P and f = ([t >= P] R - m) mod P.
 template <int K>
 XHE_DEV void pmd_from_mont2(const PMD<K>& M, const uint32_t (&X)[2 * K], const uint32_t* RmodP, uint32_t (&e)[K],
                             uint32_t (&f)[K]) {
-  uint64_t T[2 * K];
-  uint32_t m[K], P[K], u[K];
+  uint32_t m[K];
+  {
+    uint64_t T[2 * K];
 #pragma unroll
-  for (int j = 0; j < 2 * K; ++j) T[j] = X[j];
-#pragma unroll
-  for (int j = 0; j < K; ++j) P[j] = M.p[j];
-  pmd_redc_wide<K>(M, T, e, m);
-  uint32_t d[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) d[j] = e[j];
-  const bool ge = pmd_sub<K>(d, P) == 0;  // t >= P
-#pragma unroll
-  for (int j = 0; j < K; ++j) e[j] = ge ? d[j] : e[j];
-  // m mod P = REDC(m * (R mod P))
-#pragma unroll
-  for (int j = 0; j < 2 * K; ++j) T[j] = 0;
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const uint32_t ri = RmodP[i];
-#pragma unroll
-    for (int j = 0; j < K; ++j) T[i + j] = mad64(m[j], ri, T[i + j]);
+    for (int j = 0; j < 2 * K; ++j) T[j] = X[j];
+    pmd_redc_wide<K>(M, T, e, m);
   }
-  uint32_t q[K];
-  pmd_redc_wide<K>(M, T, u, q);
+  __builtin_amdgcn_sched_barrier(0);
+  const bool ge = pmd_csub<K>(M, e);  // t >= P
+  __builtin_amdgcn_sched_barrier(0);
+  pmd_mod_small<K>(M, m);
+  __builtin_amdgcn_sched_barrier(0);
+  // f = (ge ? R mod P : 0) - (m mod P), plus P on a borrow
+  int64_t br = 0;
 #pragma unroll
-  for (int j = 0; j < K; ++j) d[j] = u[j];
-  if (pmd_sub<K>(d, P) == 0) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) u[j] = d[j];
+  for (int j = 0; j < K; ++j) {
+    const int64_t v = (int64_t)(ge ? RmodP[j] : 0u) - (int64_t)m[j] + br;
+    f[j] = (uint32_t)v & ((1u << 28) - 1u);
+    br = v >> 28;
   }
-  // f = (ge ? R mod P : 0) - u  (mod P)
-#pragma unroll
-  for (int j = 0; j < K; ++j) f[j] = ge ? RmodP[j] : 0u;
-  if (pmd_sub<K>(f, u)) {
+  if (br) {
     int64_t cy = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const int64_t v = (int64_t)f[j] + (int64_t)P[j] + cy;
+      const int64_t v = (int64_t)f[j] + (int64_t)M.p[j] + cy;
       f[j] = (uint32_t)v & ((1u << 28) - 1u);
       cy = v >> 28;
     }

@@ -395,8 +395,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o.qinvpR = bl.put_limbs(mulmod(modinv(Q, P), Rp, P), s1);  // context.py:43
     o.q_lim = bl.put_limbs(Q, s1);
 #if XHE_PMD && XHE_LDS_ROWS
-    if (k->djn && K == 2048) {
-      // Montgomery-digit encryption (k_djn_pmd): MASK + E_i, E = (1 - R) mod P,
+    if (K == 2048) {
+      // Montgomery-digit kernels (k_djn_pmd, k_dec_pmd): MASK + E_i, E = (1 - R) mod P,
       // R = 2^(28*37) (= the mod-p shape's R, so R mod P is kd.p.R1)
       auto topc = [&](const BigU& X) {
         std::vector<uint32_t> v = submod(BigU(1), mod(T, X), X).to_limbs(28, 37);
@@ -473,6 +473,12 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.eq_words = B + o.eq;
     kd.ep_bits = ep_bits;
     kd.eq_bits = eq_bits;
+#if XHE_PMD && XHE_LDS_ROWS
+    if (K == 2048) {
+      kd.topc_p = B + o.topc_p;
+      kd.topc_q = B + o.topc_q;
+    }
+#endif
     if (k->djn) {
       kd.win = win & 0xff;
       win_layout(k->rand_bits, kd.win, (win & XHE_WIN_SPLIT) != 0, &kd.nwin, &kd.nhi);
@@ -499,8 +505,6 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       if (K == 2048) {
         // rows as Montgomery digits (e, f) for k_djn_pmd
         kd.pmd = 1;
-        kd.topc_p = B + o.topc_p;
-        kd.topc_q = B + o.topc_q;
         const int64_t trows = (int64_t)(kd.nwin + kd.nhi) << kd.win;
         const ModDev mp[2] = {kd.p, kd.q};
         for (int i = 0; i < 2; ++i) {
@@ -1065,6 +1069,34 @@ void dec_pow_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
   ws_free(ws, s);
 }
 
+#if XHE_PMD && XHE_LDS_ROWS
+// one lane per residue, exponentiation in Montgomery digits (2048-bit keys)
+template <class MP2>
+void dec_pmd_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chunk, uint32_t* xrows, hipStream_t s) {
+  constexpr int NQ = PMD<37>::NQ;
+  const int pow_blocks = (int)std::min<int64_t>((chunk + 127) / 128, 1024);
+  const int64_t lanes = (int64_t)pow_blocks * 128;
+  uint4 *ws = nullptr, *st = nullptr;
+  ws_alloc((void**)&ws, (size_t)2 * 16 * NQ * lanes * sizeof(uint4), s);
+  ws_alloc((void**)&st, (size_t)2 * NQ * chunk * sizeof(uint4), s);
+  const dim3 g1((unsigned)((n + 127) / 128), 2);
+  hipLaunchKernelGGL((k_dec_pmd_in<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                     k->kd.q2.N, ct, n, st);
+  HIPCHK(hipGetLastError());
+  {
+    ProfScope ps("k_dec_pow", s);
+    hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3(pow_blocks, 2), dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, n, st,
+                       ws);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL((k_dec_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                     k->kd.q2.N, n, st, (int)MP2::S4, xrows);
+  HIPCHK(hipGetLastError());
+  ws_free(ws, s);
+  ws_free(st, s);
+}
+#endif
+
 template <class Sh>
 void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -1086,6 +1118,9 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
     const uint32_t* cto = ct + (size_t)off * k->n2w;
     if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
     else if (tpi == 4) dec_pow_launch<typename Sh::MP2L, 1, MP2>(k, cto, n, chunk, xrows, s);
+#if XHE_PMD && XHE_LDS_ROWS
+    else if constexpr (Sh::K == 2048) dec_pmd_launch<MP2>(k, cto, n, chunk, xrows, s);
+#endif
     else dec_pow_launch<MP2, 0, MP2>(k, cto, n, chunk, xrows, s);
     int blocks = (int)((n * MP::TPI + 255) / 256);
     hipLaunchKernelGGL((k_dec_fin<MP2, MP>), dim3(blocks, 2), dim3(256), 0, s, k->kd, k->kd.p.N, k->kd.q.N, n,

@@ -666,6 +666,268 @@ __global__ void __launch_bounds__(128, 2) k_djn_pmd(KeyDev key, const uint32_t* 
   N.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
 
+// x <- x^E mod P^2 in Montgomery digits for an exponent E shared by every
+// lane (P - 1: the schedule is wave-uniform): 5-bit sliding window as
+// pow_uniform_exp, odd powers x^(2t+1), t < 16, in this lane's column of a
+// global table (entry t, quad q at tab[(t NQ + q) G], interleaved limb
+// pairs). Every product reads its second operand from the lane's LDS slot:
+// a squaring parks the state there, a table product copies the entry there
+// (19 loads in flight at once); squarings take PMD::sqr (4 K^2 mads).
+// (tab: the table's uniform base, lane: this lane's column, G columns; the
+// per-lane address is formed at each use, not held across the products)
+template <int KP>
+XHE_DEV void pmd_pow_uniform(const PMD<KP>& M, uint32_t (&a)[KP], uint32_t (&c)[KP], const uint32_t* ex, int ebits,
+                             uint4* __restrict__ tab_base, int lane, int G, uint32_t* slot, const uint32_t* topc) {
+  constexpr int NQ = PMD<KP>::NQ;
+#define tab (tab_base + opaque_i(lane))
+  auto quad = [&](int q) -> uint4 {
+    return make_uint4(2 * q < KP ? a[2 * q] : 0u, 2 * q < KP ? c[2 * q] : 0u, 2 * q + 1 < KP ? a[2 * q + 1] : 0u,
+                      2 * q + 1 < KP ? c[2 * q + 1] : 0u);
+  };
+  auto put_slot = [&]() XHE_INL {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) *reinterpret_cast<uint4*>(slot + q * 256) = quad(q);
+  };
+  auto put_tab = [&](int t) XHE_INL {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tab[((size_t)t * NQ + q) * G] = quad(q);
+  };
+  auto tab_to_slot = [&](int t) XHE_INL {
+    uint4 v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = tab[((size_t)t * NQ + q) * G];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) *reinterpret_cast<uint4*>(slot + q * 256) = v[q];
+  };
+  auto tab_to_regs = [&](int t) XHE_INL {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint4 v = tab[((size_t)t * NQ + q) * G];
+      if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+      if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+    }
+  };
+  auto bit = [&](int i) { return (ex[i >> 5] >> (i & 31)) & 1u; };
+  int i = ebits - 1;
+  while (i >= 0 && !bit(i)) --i;
+  int pend_sq = 0, pend_mul = -1;
+  bool sq = false;  // the next product is a squaring (PMD::sqr) of the parked state
+  // the next product of the window schedule: its operand into the slot
+  auto next_op = [&]() -> bool {
+    while (true) {
+      if (pend_sq > 0) {
+        put_slot();
+        --pend_sq;
+        sq = true;
+        return true;
+      }
+      if (pend_mul >= 0) {
+        tab_to_slot(pend_mul);
+        pend_mul = -1;
+        sq = false;
+        return true;
+      }
+      if (i < 0) return false;
+      if (!bit(i)) {
+        pend_sq = 1;
+        --i;
+      } else {
+        int j = i - 4 < 0 ? 0 : i - 4;
+        while (!bit(j)) ++j;  // window [i..j] ends in a set bit
+        uint32_t val = 0;
+        for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+        pend_sq = i - j + 1;
+        pend_mul = (int)(val >> 1);
+        i = j - 1;
+      }
+    }
+  };
+  // Products in order: x x -> x^2 (then the slot keeps x^2 and the state
+  // returns to x), x^(2t-1) x^2 -> tab[t] for t = 1..15, then the window
+  // schedule - all through ONE inlined product.
+  put_tab(0);
+  put_slot();
+  sq = true;
+  int t = -1;
+#pragma unroll 1
+  while (true) {
+    if (sq) M.sqr(a, c, slot, topc);
+    else M.mul(a, c, slot, topc);
+    if (t < 15) {
+      sq = false;
+      if (t < 0) {
+        put_slot();
+        tab_to_regs(0);
+      } else {
+        put_tab(t + 1);
+      }
+      ++t;
+      if (t < 15) continue;
+      // first window of the exponent: its odd power is the start value
+      int j = i - 4 < 0 ? 0 : i - 4;
+      while (!bit(j)) ++j;
+      uint32_t val = 0;
+      for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+      tab_to_regs((int)(val >> 1));
+      i = j - 1;
+    }
+    if (!next_op()) break;
+  }
+#undef tab
+}
+
+// k_dec_pow (one lane per residue) in Montgomery digits, as three kernels so
+// that each has the registers to itself: k_dec_pmd_in (c -> c R^2 mod P^2 by
+// the 74-limb REDC and a product by R^3, then its digits, pmd_from_mont2),
+// k_dec_pmd_pow (x^(P-1) in digits) and k_dec_pmd_out (back through R a + P c
+// and one Montgomery product by 1; X_P = x - 1 written to xrows
+// [prime][xs4][count] exactly as k_dec_pow<MP2, 0>). The digit state between
+// them: st [prime][NQ quads][count] uint4 (interleaved limb pairs).
+template <class MP2, int KP>
+__global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_t* __restrict__ Pp,
+                                                       const uint32_t* __restrict__ Pq,
+                                                       const uint32_t* __restrict__ Np2,
+                                                       const uint32_t* __restrict__ Nq2,
+                                                       const uint32_t* __restrict__ c_words, int64_t count,
+                                                       uint4* __restrict__ st) {
+  static_assert(MP2::TPI == 1 && MP2::S == 2 * KP && MP2::W == 28, "digits of the one-lane P^2 shape");
+  constexpr int NQ = PMD<KP>::NQ;
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
+  const int prime = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  uint32_t* slot = img_all[(threadIdx.x >> 6) & 1] + (threadIdx.x & 63) * 4;
+  const int n2w = key.n2w;
+  const uint32_t* cw = c_words + (size_t)e * n2w;
+  uint32_t x[MP2::L];
+  {
+    MP2 N;
+    N.init(prime ? Nq2 : Np2, md.n0inv);
+    // high limbs [S, 2S) of c into the slot (the REDC's upper-half source)
+#pragma unroll
+    for (int q = 0; q < MP2::S4 / 4; ++q) {
+      uint32_t v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int J = MP2::S + 4 * q + r, bit = MP2::W * J, k = bit >> 5, sh = bit & 31;
+        const uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+        v[r] = 4 * q + r < MP2::S ? (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2::MASK : 0u;
+      }
+      *reinterpret_cast<uint4*>(slot + q * 256) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    N.load_words(x, cw, n2w);  // low S limbs
+    N.redc_wide(x, ALdsQ{slot});
+    N.mul(x, ARow{md.R3});  // c R^2 mod P^2 (< 2 P^2)
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  PMD<KP> M;
+  M.init(prime ? Pq : Pp, prime ? key.q.n0inv : key.p.n0inv);
+  uint32_t a[KP], c[KP];
+  pmd_from_mont2<KP>(M, x, prime ? key.q.R1 : key.p.R1, a, c);
+  uint4* so = st + (size_t)prime * NQ * count + e;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    so[(size_t)q * count] = make_uint4(2 * q < KP ? a[2 * q] : 0u, 2 * q < KP ? c[2 * q] : 0u,
+                                       2 * q + 1 < KP ? a[2 * q + 1] : 0u, 2 * q + 1 < KP ? c[2 * q + 1] : 0u);
+}
+
+template <int KP>
+__global__ void __launch_bounds__(128, 2) k_dec_pmd_pow(KeyDev key, const uint32_t* __restrict__ Pp,
+                                                        const uint32_t* __restrict__ Pq, int64_t count,
+                                                        uint4* __restrict__ st, uint4* __restrict__ ws) {
+  using D = PMD<KP>;
+  constexpr int NQ = D::NQ;
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][NQ * 256];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[(KP + 3) & ~3];
+  const int prime = blockIdx.y;
+  const uint32_t* tcg = prime ? key.topc_q : key.topc_p;
+  if (threadIdx.x < KP) topc[threadIdx.x] = tcg[threadIdx.x];
+  __syncthreads();
+  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
+  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
+  // 32-bit indices (count < 2^31 per launch), per-lane addresses formed at
+  // use: the product needs every register it can get
+  const int G = (int)(gridDim.x * blockDim.x);
+  const int gid0 = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  uint4* tab = ws + (size_t)prime * 16 * NQ * G;
+  uint4* stp = st + (size_t)prime * NQ * count;
+  uint32_t* slot = img_all[(threadIdx.x >> 6) & 1] + (threadIdx.x & 63) * 4;
+  D M;
+  M.init(prime ? Pq : Pp, prime ? key.q.n0inv : key.p.n0inv);
+  for (int e = gid0; e < (int)count; e += G) {
+    uint32_t a[KP], c[KP];
+    {
+      const uint4* se = stp + e;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const uint4 v = se[(size_t)q * count];
+        if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+        if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+      }
+    }
+    pmd_pow_uniform<KP>(M, a, c, ex, ebits, tab, gid0, G, slot, topc);
+    uint4* so = stp + opaque_i(e);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      so[(size_t)q * count] = make_uint4(2 * q < KP ? a[2 * q] : 0u, 2 * q < KP ? c[2 * q] : 0u,
+                                         2 * q + 1 < KP ? a[2 * q + 1] : 0u, 2 * q + 1 < KP ? c[2 * q + 1] : 0u);
+  }
+}
+
+template <class MP2, int KP>
+__global__ void __launch_bounds__(128, 2) k_dec_pmd_out(KeyDev key, const uint32_t* __restrict__ Pp,
+                                                        const uint32_t* __restrict__ Pq,
+                                                        const uint32_t* __restrict__ Np2,
+                                                        const uint32_t* __restrict__ Nq2, int64_t count,
+                                                        const uint4* __restrict__ st, int xs4,
+                                                        uint32_t* __restrict__ xrows) {
+  constexpr int NQ = PMD<KP>::NQ;
+  const int prime = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const uint4* se = st + (size_t)prime * NQ * count + e;
+  uint32_t a[KP], c[KP], x[MP2::L];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const uint4 v = se[(size_t)q * count];
+    if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+    if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+  }
+  {
+    PMD<KP> M;
+    M.init(prime ? Pq : Pp, prime ? key.q.n0inv : key.p.n0inv);
+    M.to_mont2(a, c, x);  // x^(P-1) R^2 mod P^2, unreduced
+  }
+  // out of Montgomery form: 1 * X R^-2 with X streamed from the lane's LDS
+  // slot (as k_djn_pmd's last product)
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
+  uint32_t* slot = img_all[(threadIdx.x >> 6) & 1] + (threadIdx.x & 63) * 4;
+#pragma unroll
+  for (int q = 0; q < MP2::S4 / 4; ++q)
+    *reinterpret_cast<uint4*>(slot + q * 256) =
+        make_uint4(4 * q < MP2::S ? x[4 * q] : 0u, 4 * q + 1 < MP2::S ? x[4 * q + 1] : 0u,
+                   4 * q + 2 < MP2::S ? x[4 * q + 2] : 0u, 4 * q + 3 < MP2::S ? x[4 * q + 3] : 0u);
+  wave_sync_mem_();
+  __builtin_amdgcn_sched_barrier(0);  // keep the phases apart (interleaved, they spill)
+#pragma unroll
+  for (int j = 0; j < MP2::L; ++j) x[j] = j == 0 ? 1u : 0u;
+  MP2 N;
+  N.init(prime ? Nq2 : Np2, prime ? key.q2.n0inv : key.p2.n0inv);
+  N.mul(x, ALdsQ{slot});
+  N.reduce_once(x);  // c^(P-1) mod P^2, = 1 (mod P)
+  // X = x - 1 (x >= 1): a 32-bit borrow chain (the 64-bit add-all-ones form
+  // of k_dec_pow spills here)
+  uint32_t br = 1u;
+  uint32_t* xo = xrows + (size_t)prime * xs4 * count + e;
+#pragma unroll
+  for (int j = 0; j < MP2::L; ++j) {
+    const uint32_t v = x[j] - br;
+    br = x[j] < br ? 1u : 0u;
+    xo[(size_t)j * count] = v & MP2::MASK;
+  }
+}
+
 // Rewrite packed fixed-base table rows X = x R^2 mod P^2 (the 74-limb
 // Montgomery form k_tab_combine writes, RW words) as their Montgomery digits
 // (e, f) < P, RW/2 words each (pdigit_dev.hpp pmd_from_mont2). One thread per
