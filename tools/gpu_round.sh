@@ -3,7 +3,7 @@
 # passes. Ordinary test failures (pytest exit 1) do not stop the script; a
 # crash, abort or time limit of any GPU step does (nothing else runs on the
 # GPU after it).
-#   tools/gpu_round.sh TAG [tests|bench|prof ...]   (default: tests bench)
+#   tools/gpu_round.sh TAG [tests|smoke|bench|prof|lr ...]   (default: tests bench)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r2}
 shift
@@ -29,6 +29,10 @@ for s in $STEPS; do
       ;;
     prof)
       bash tools/profile_box.sh "$TAG/prof" || exit $?
+      ;;
+    lr)
+      timeout -k 10 600 python -u tools/lr_he_demo.py --epochs 3 --check > "$OUT/lr_demo.json" 2> "$OUT/lr_demo.err" || { tail -20 "$OUT/lr_demo.err"; exit 3; }
+      tail -c 1500 "$OUT/lr_demo.json"
       ;;
     *)
       echo "unknown step $s"; exit 2
