@@ -212,7 +212,11 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
     for tag, args_ in (("encrypt_public_nodjn_per_s", (None, None, None)),
                        ("encrypt_public_djn_per_s", (None, None, h_)),
                        ("encrypt_private_nodjn_per_s", (p_, q_, None))):
-        k2 = nat.DeviceKey(dk.key_bits, n_, *args_, device=dk.device, win_bits=8 if args_[2] else 0)
+        # public DJN at the drop-in's window (a public key's DeviceKey takes the
+        # library default, 16: 64 windows of 2^16 rows mod n^2, 2.1 GB)
+        k2 = nat.DeviceKey(dk.key_bits, n_, *args_, device=dk.device, win_bits=16 if args_[2] else 0)
+        if args_[2]:
+            out["encrypt_public_djn_window_bits"] = 16
         nat.check(L.xhe_rand(k2.handle, b"\x01" * 32, 5, nm, rk.data_ptr(), None, stream), "rand")
         t = _timed(lambda: nat.check(L.xhe_encrypt(k2.handle, m.data_ptr(), rk.data_ptr(), nm, ctm.data_ptr(), stream),
                                      tag), reps=2)
@@ -234,46 +238,78 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
                                                            None), "decrypt_host"), reps=2)
     out["decrypt_decode_host_buffers_per_s"] = nh / t
     out["host_roundtrip_max_abs_err"] = float(np.max(np.abs(f64 - xh)))
-    # the same through the drop-in API (what XFL's operators call): the label
-    # trainer's Paillier.encrypt(float32[]) -> Paillier.serialize, and the
-    # receiving side's ciphertext_from -> Paillier.decrypt
-    # (logistic_regression/label_trainer.py:193-199, 258); the context uses
-    # this run's key handle (same tables)
+    return out
+
+
+def measure_dropin(nat, device, key_bits, xh, key_material):
+    """The same through the drop-in API (what XFL's operators call), with the
+    drop-in's own PaillierContext - its window policy (window 16 first, wider
+    as the key's encrypted volume grows, context.py WIN_STEPS) and its
+    device-resident arrays (xfl_amd/paillier/resident.py): the label trainer's
+    Paillier.encrypt(float32[]) -> Paillier.serialize, the receiving side's
+    ciphertext_from -> Paillier.decrypt (logistic_regression/label_trainer.py:
+    193-199, 258), config 3's pairwise sum, and the LR step's encrypt ->
+    np.matmul -> serialize chain (logistic_regression/trainer.py:166). Each
+    figure carries the fixed-base window the context's key had after it."""
+    import gc
+    import torch
     from xfl_amd.paillier import Paillier, PaillierContext
-    # one GPU's rates: the drop-in would otherwise spread each call over every
-    # visible GPU (num_cores=-1, the reference's default), e.g. all 8 of a node
-    os.environ["XHE_DEVICES"] = str(dk.device)
+    out = {}
+    p_, q_, n_, h_ = key_material
+    nh = xh.shape[0]
+    # one GPU's rates: pin the drop-in to this rank's GPU
+    os.environ["XHE_DEVICES"] = str(device)
     ctx = PaillierContext().init(p_, q_, djn_h_pow_n=h_)
-    ctx._dev = {dk.device: dk}
+    win = {}
+
+    def note(tag):  # the window of the key the last call used (no rebuild here)
+        win[tag] = ctx._dev[device].win_bits
+        ctx._volume = 0  # every figure at the fresh context's window (16); the steady state is timed last
+
+    def sync():
+        torch.cuda.synchronize()
+
     x32 = xh.astype(np.float32)
     wire = {}
 
     def enc_ser(comp):
         wire.pop(comp, None)  # the previous payload is released first, as in a training loop
         wire[comp] = Paillier.serialize(Paillier.encrypt(ctx, x32, precision=7), compression=comp)
-    t = _timed(lambda: enc_ser(False), reps=3)
-    out["dropin_encrypt_serialize_per_s"] = nh / t
     enc = {}
 
     def enc_only():
         enc.pop(0, None)
         enc[0] = Paillier.encrypt(ctx, x32, precision=7)
+        sync()
     out["dropin_encrypt_per_s"] = nh / _timed(enc_only, reps=3)
+    note("dropin_encrypt_per_s")
+    out["dropin_encrypt_resident"] = bool(enc[0].is_resident)
     ser = {}
 
     def ser_only():
         ser.pop(0, None)
+        enc[0]._st.h = None  # a fresh encryption's words are only in HBM: serialize includes the download
         ser[0] = Paillier.serialize(enc[0], compression=False)
     out["dropin_serialize_per_s"] = nh / _timed(ser_only, reps=3)
-    # config 3's pairwise sum through the API: PaillierArray + PaillierArray
-    # (paillier.py:88-123 per element; host buffers in and out)
+    t = _timed(lambda: enc_ser(False), reps=3)
+    out["dropin_encrypt_serialize_per_s"] = nh / t
+    note("dropin_encrypt_serialize_per_s")
+    # config 3's pairwise sum: PaillierArray + PaillierArray on resident operands
     tot = {}
 
     def add_only():
         tot.pop(0, None)
         tot[0] = enc[0] + enc[0]
+        sync()
     out["dropin_add_per_s"] = nh / _timed(add_only, reps=3)
-    del enc, ser, tot
+    out["dropin_add_resident"] = bool(tot[0].is_resident and tot[0]._st.h is None)
+    # decrypt of a resident array (only the float32 results come back)
+    out["dropin_decrypt_resident_per_s"] = nh / _timed(lambda: Paillier.decrypt(ctx, tot[0]), reps=2)
+    back2 = Paillier.decrypt(ctx, tot[0])
+    out["dropin_add_max_abs_err"] = float(np.max(np.abs(back2 - 2 * x32.astype(np.float64))))
+    ser.clear()
+    tot.clear()
+    gc.collect()
     t = _timed(lambda: Paillier.decrypt(ctx, Paillier.ciphertext_from(None, wire[False], compression=False)), reps=2)
     out["dropin_deserialize_decrypt_per_s"] = nh / t
     t = _timed(lambda: Paillier.ciphertext_from(None, wire[False], compression=False), reps=3)
@@ -282,8 +318,71 @@ def measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, key_material):
     out["dropin_roundtrip_max_abs_err"] = float(np.max(np.abs(back - x32)))
     t = _timed(lambda: enc_ser(True), reps=1)
     out["dropin_encrypt_serialize_zstd_per_s"] = nh / t
+    note("dropin_encrypt_serialize_zstd_per_s")
     out["wire_bytes_per_ciphertext"] = len(wire[False]) / nh
+    # the LR step (B = 2048 residuals, D = 15 features): encrypt -> matmul -> serialize
+    rng = np.random.default_rng(11)
+    r = rng.standard_normal(2048).astype(np.float32)
+    X = rng.standard_normal((2048, 15))
+    chain = {}
+
+    def lr_chain():
+        chain[0] = Paillier.serialize(Paillier.encrypt(ctx, r, precision=7) @ X)
+    out["dropin_chain_encrypt_matmul_serialize_2048x15_s"] = _timed(lr_chain, reps=5)
+    got = Paillier.decrypt(ctx, Paillier.ciphertext_from(ctx, chain[0]))
+    out["dropin_chain_max_abs_err"] = float(np.max(np.abs(got - r.astype(np.float64) @ X)))
+    note("dropin_chain_encrypt_matmul_serialize_2048x15_s")
+    out["dropin_table_bytes_w16"] = nat.table_bytes(key_bits, 16)
+    # the policy's steady state for a loop of 1 M-element calls: past 64 M
+    # encrypted elements the key's tables are rebuilt at window 22 (when they
+    # leave 32 GiB free; the rebuild happens in the untimed first call)
+    ctx._volume = ctx.WIN_STEPS[-1][0]
+    out["dropin_encrypt_steady_per_s"] = nh / _timed(enc_only, reps=3)
+    win["dropin_encrypt_steady_per_s"] = ctx._dev[device].win_bits
+    out["dropin_table_bytes_steady"] = nat.table_bytes(key_bits, ctx._dev[device].win_bits)
+    out["dropin_window_bits"] = win
+    wire.clear()
+    enc.clear()
+    ctx._dev = {}
+    gc.collect()
+    torch.cuda.empty_cache()
     return out
+
+
+def headline_at_window(nat, L, bits, key_material, win, x, m, ex, st, rnd, N, stream, steps):
+    """The headline step (encode + draw + encrypt of N resident float64) on a
+    key with `win`-bit tables: the drop-in's starting window is 16
+    (context.py WIN_STEPS), so this is what an XFL caller's first calls get."""
+    import ctypes
+    import torch
+    p, q, n, h = key_material
+    k = nat.DeviceKey(bits, n, p, q, h, device=torch.cuda.current_device(), win_bits=win)
+    ct = torch.empty((N, k.n2w), dtype=torch.int32, device="cuda")
+    seed32 = os.urandom(32)
+
+    def step(i):
+        nat.check(L.xhe_encode_f64(k.handle, x.data_ptr(), N, 7, 0, 0, m.data_ptr(), ex.data_ptr(), st.data_ptr(),
+                                   stream), "encode")
+        nat.check(L.xhe_rand(k.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
+        nat.check(L.xhe_encrypt(k.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
+    step(0)
+    torch.cuda.synchronize()
+    L.xhe_profile(1)
+    t0 = time.time()
+    for i in range(steps):
+        step(i + 1)
+    torch.cuda.synchronize()
+    wall = time.time() - t0
+    tot, cnt = ctypes.c_double(), ctypes.c_int64()
+    nat.check(L.xhe_profile_read(b"k_djn_pow", ctypes.byref(tot), ctypes.byref(cnt)))
+    L.xhe_profile(0)
+    _, w_pow = algorithmic_macs_per_element(bits, win, k.rand_bits)
+    avg = tot.value / max(cnt.value, 1) / 1e3
+    rec = {"window_bits": win, "value": N * steps / wall, "unit": "encrypts/s", "ms_per_step": wall / steps * 1e3,
+           "kernel_avg_ms": avg * 1e3, "frac": N * w_pow / avg / PEAK_MAC_PER_S,
+           "table_bytes": nat.table_bytes(bits, win)}
+    del k, ct
+    return rec
 
 
 def host_cores():
@@ -449,8 +548,20 @@ def main():
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,
         }
+        rec["config"]["table_bytes"] = nat.table_bytes(bits, args.win)
+        if not args.no_ops and (args.win & 0xFF) != 16:
+            rec["headline_dropin_window"] = headline_at_window(nat, L, bits, (p, q, n, h), 16, x, m, ex, st, rnd, N,
+                                                               stream, args.steps)
         if not args.no_ops:
             rec["ops"] = measure_ops(nat, L, dk, x, m, ex, ct, rnd, N, stream, (p, q, n, h))
+            # the drop-in with its own context and window policy: the bench
+            # key's tables (193 GB at window 23) are released first
+            dev, xh = dk.device, x[:min(N, 1 << 20)].cpu().numpy()
+            del pipe, encrypt_shard, dk
+            import gc
+            gc.collect()
+            torch.cuda.empty_cache()
+            rec["ops"].update(measure_dropin(nat, dev, bits, xh, (p, q, n, h)))
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baselines(bits, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

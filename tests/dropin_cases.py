@@ -30,7 +30,8 @@ def raw(arr):
 def ops_bit_exact(fx, vectorized):
     """vectorized=False: numpy's per-element object loop over PaillierCiphertext
     operators; True: PaillierArray's batched kernels (segmented product,
-    batch inversion, multi-exponentiation matmul)."""
+    batch inversion, multi-exponentiation matmul); "resident": the same with
+    the operands held in HBM (every result stays there; GPU only)."""
     from xfl_amd.paillier import PaillierArray
     g = load_fixture(fx)
     priv, pub = ctxs(g)
@@ -39,6 +40,9 @@ def ops_bit_exact(fx, vectorized):
     b = cts(pub, ops["b"])
     if vectorized:
         a, b = PaillierArray(a), PaillierArray(b)
+        if vectorized == "resident":
+            a.to_device(), b.to_device()
+            assert a.is_resident and (a + b).is_resident and (a * 2.5).is_resident
     sc = [fl(s) if isinstance(s, str) else s for s in ops["mul_pub"]["scalar"]]
     want = lambda name: ([hx(r) for r in ops[name]["raw"]], ops[name]["exp"])  # noqa: E731
     assert raw(a + b) == want("add")
@@ -145,8 +149,10 @@ def wire_roundtrip(fx):
     assert [o.value for o in obj] == [hx(r) for r in g["ops"]["a"]["raw"][:4]]
 
 
-def array_protocol(fx):
-    """The ndarray surface the operators use on encrypted arrays."""
+def array_protocol(fx, resident=False):
+    """The ndarray surface the operators use on encrypted arrays (resident:
+    the array's words held in HBM first, so views, takes, copies and
+    assignments go through the device copy)."""
     import pandas as pd
 
     from xfl_amd.paillier import Paillier, PaillierArray, PaillierCiphertext
@@ -154,6 +160,9 @@ def array_protocol(fx):
     priv, pub = ctxs(g)
     a_obj = cts(pub, g["ops"]["a"])  # 16 ciphertexts, mixed exponents
     a = PaillierArray(a_obj)
+    if resident:
+        a.to_device()
+        a._st.h = None  # device copy only: every host read below downloads
     R, E = raw(a_obj)
     assert a.shape == (16,) and a.ndim == 1 and a.size == 16 and len(a) == 16 and a.dtype == object
     assert isinstance(a[3], PaillierCiphertext) and (a[3].raw_ciphertext, a[3].exponent) == (R[3], E[3])
@@ -259,6 +268,8 @@ def gap_alignment(fx, vectorized):
     scale = fl(ops["gap"]["scale"])
     if vectorized:
         A = PaillierArray(cg)
+        if vectorized == "resident":
+            A.to_device()
         first = A[:1] * scale * scale
         assert raw(first) == ([want("gap_operands")[0][0]], [want("gap_operands")[1][0]])
     else:
@@ -270,6 +281,8 @@ def gap_alignment(fx, vectorized):
         gc = cts(ctx, ops["gap_operands"])
         if vectorized:
             A = PaillierArray(gc)
+            if vectorized == "resident":
+                A.to_device()
             got = A[li] + A[ri]
         else:
             got = np.array([gc[i] + gc[j] for i, j in pairs], dtype=object)
@@ -278,6 +291,8 @@ def gap_alignment(fx, vectorized):
     orders = ops["gap_sum"]["orders"]
     if vectorized:
         A = PaillierArray(gc)
+        if vectorized == "resident":
+            A.to_device()
         sums = [np.sum(A[o]) for o in orders]
     else:
         sums = [np.sum(gc[o]) for o in orders]

@@ -179,3 +179,22 @@ def test_window_layouts():
 @pytest.mark.parametrize("fx", HOST_FIXTURES)
 def test_gap_alignment_negative_branch(fx, vectorized):
     C.gap_alignment(fx, vectorized)
+
+
+def test_shifted_words_matches_python_ints():
+    import numpy as np
+    """the aligned mat-vec exponents k << shift built with numpy equal the
+    Python-int construction (and kbits bounds every value)"""
+    from xfl_amd._native import words_to_ints
+    from xfl_amd.paillier.array import _shifted_words
+    rng = np.random.default_rng(0)
+    for t in range(200):
+        n = int(rng.integers(1, 40))
+        k = rng.integers(0, 2 ** 63, size=n, dtype=np.int64) >> rng.integers(0, 63, size=n)
+        if t % 5 == 0:
+            k[1:] = 0
+        s = rng.integers(0, 200, size=n)
+        w, kbits = _shifted_words(k, s)
+        want = [int(a) << int(b) for a, b in zip(k, s)]
+        assert words_to_ints(w) == want
+        assert max(v.bit_length() for v in want) <= kbits

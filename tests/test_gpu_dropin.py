@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 from tests import dropin_cases as C
 
 
-@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("vectorized", [False, True, "resident"])
 @pytest.mark.parametrize("fx", FIXTURES)
 def test_ops_bit_exact(fx, vectorized):
     C.ops_bit_exact(fx, vectorized)
@@ -28,7 +28,7 @@ def test_histogram_groupby_bit_exact():
     C.histogram_groupby(FIXTURES[0])
 
 
-@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("vectorized", [False, True, "resident"])
 @pytest.mark.parametrize("fx", ["paillier_2048_djn.json", "paillier_2048_nodjn.json"])
 def test_gap_alignment_negative_branch(fx, vectorized):
     """device alignment across gaps >= the negative-branch threshold:
@@ -75,9 +75,10 @@ def test_wire_roundtrip_with_reference_pickles(fx):
     C.wire_roundtrip(fx)
 
 
+@pytest.mark.parametrize("resident", [False, True])
 @pytest.mark.parametrize("fx", FIXTURES[:2])
-def test_array_protocol(fx):
-    C.array_protocol(fx)
+def test_array_protocol(fx, resident):
+    C.array_protocol(fx, resident)
 
 
 @pytest.mark.parametrize("fx", FIXTURES)

@@ -30,7 +30,8 @@ import numbers
 import numpy as np
 
 from .. import _native as nat
-from . import ops
+from . import ops, resident
+from .resident import Rows
 
 
 def _ct_type():
@@ -54,7 +55,8 @@ class PaillierArray:
         """PaillierArray(ciphertexts): from an object array / nested list of
         PaillierCiphertext (one key), or another PaillierArray (copy)."""
         if isinstance(obj, PaillierArray):
-            self._set(obj.context, obj._w.copy(), obj._e.copy(), obj._shape)
+            c = obj.copy()
+            self._set(c.context, c._st, c._lo, c._e, c._shape)
             return
         arr = np.asarray(obj, dtype=object)
         flat = arr.reshape(-1)
@@ -76,11 +78,11 @@ class PaillierArray:
         n2w = _n2w(ctx, raws)
         w = nat.ints_to_words(raws, n2w) if raws else np.zeros((0, n2w), dtype=np.uint32)
         e = np.fromiter((c.exponent for c in flat), dtype=np.int32, count=flat.size)
-        self._set(ctx, np.ascontiguousarray(w), e, arr.shape)
+        self._set(ctx, Rows(h=np.ascontiguousarray(w)), 0, e, arr.shape)
 
     @classmethod
     def from_buffers(cls, context, words, exps, shape=None):
-        """Wrap flat buffers (no copy when already uint32/int32 C-contiguous)."""
+        """Wrap flat host buffers (no copy when already uint32/int32 C-contiguous)."""
         self = cls.__new__(cls)
         words = np.ascontiguousarray(words, dtype=np.uint32)
         exps = np.ascontiguousarray(exps, dtype=np.int32).reshape(-1)
@@ -88,23 +90,79 @@ class PaillierArray:
             shape = (exps.shape[0],)
         if words.ndim != 2:
             words = words.reshape(exps.shape[0], -1) if exps.shape[0] else np.zeros((0, 1), dtype=np.uint32)
-        self._set(context, words, exps, tuple(int(s) for s in shape))
+        self._set(context, Rows(h=words), 0, exps, tuple(int(s) for s in shape))
         return self
 
-    def _set(self, ctx, w, e, shape):
+    @classmethod
+    def from_device(cls, context, dwords, exps, shape=None):
+        """Wrap device words (an int32 tensor [size, n2w] in HBM, resident.py)
+        and host exponents; the host copy is made on first host access."""
+        self = cls.__new__(cls)
+        exps = np.ascontiguousarray(exps, dtype=np.int32).reshape(-1)
+        if shape is None:
+            shape = (exps.shape[0],)
+        self._set(context, Rows(d=dwords), 0, exps, tuple(int(s) for s in shape))
+        return self
+
+    def _set(self, ctx, st, lo, e, shape):
         shape = tuple(shape)
-        if int(np.prod(shape, dtype=np.int64)) != e.shape[0] or w.shape[0] != e.shape[0]:
-            raise ValueError(f"PaillierArray: {w.shape[0]} rows / {e.shape[0]} exponents for shape {shape}")
+        if int(np.prod(shape, dtype=np.int64)) != e.shape[0] or st.count < lo + e.shape[0]:
+            raise ValueError(f"PaillierArray: {st.count - lo} rows / {e.shape[0]} exponents for shape {shape}")
         self.context = ctx
-        self._w = w
+        self._st = st   # word storage, shared with views (resident.Rows)
+        self._lo = lo   # first row of this array in it
         self._e = e
         self._shape = shape
 
+    def _view(self, lo, e, shape):
+        """an array over rows [self._lo + lo, ...) of the same storage"""
+        v = PaillierArray.__new__(PaillierArray)
+        v._set(self.context, self._st, self._lo + lo, e, shape)
+        return v
+
+    def _whole(self):
+        return self._lo == 0 and self.size == self._st.count
+
     # ------------------------------------------------------------ buffers
     @property
+    def _w(self):
+        """host words [size, n2w] (downloaded from HBM on first use)"""
+        h = self._st.host()
+        return h if self._whole() else h[self._lo:self._lo + self.size]
+
+    def _dw(self, dev):
+        """device words [size, n2w] on `dev`: a view of the resident copy, the
+        whole buffer uploaded once (then kept), or a temporary upload of a
+        slice of a host-only buffer"""
+        if self._whole() or self._st.on_device(dev):
+            d = self._st.device(dev)
+            return d if self._whole() else d[self._lo:self._lo + self.size]
+        return resident.upload(self._w, dev)
+
+    def _resident_on(self, dev):
+        return dev is not None and self._st.on_device(dev)
+
+    def to_device(self, device=None):
+        """Keep a copy of the words in HBM of `device` (default: the
+        context's own GPU), so following batched operations run there and
+        leave their results there; returns self. No-op in host-buffer mode."""
+        dev = resident.device_for(self.context) if device is None else device
+        if dev is not None and self.size:
+            self._st.device(dev)  # the whole storage: views keep sharing it
+        return self
+
+    @property
+    def is_resident(self):
+        """whether the words are held in HBM"""
+        return self._st.d is not None
+
+    @property
     def words(self):
-        """uint32 [size, n2w] residues mod n^2 (C order over shape)"""
-        return self._w
+        """uint32 [size, n2w] residues mod n^2 (C order over shape), read-only
+        (write through arr[i] = ciphertext: the words may also live in HBM)"""
+        v = self._w.view()
+        v.flags.writeable = False
+        return v
 
     @property
     def exponents(self):
@@ -148,6 +206,9 @@ class PaillierArray:
 
     def _take(self, flat_idx, shape):
         flat_idx = np.asarray(flat_idx, dtype=np.int64).reshape(-1)
+        if self._st.d is not None:  # stays in HBM
+            d = self._st.d if self._whole() else self._st.d[self._lo:self._lo + self.size]
+            return PaillierArray.from_device(self.context, resident.take(d, flat_idx), self._e[flat_idx], shape)
         return PaillierArray.from_buffers(self.context, self._w[flat_idx], self._e[flat_idx], shape)
 
     def _index_map(self):
@@ -163,7 +224,7 @@ class PaillierArray:
             if isinstance(key, slice) and (key.step is None or key.step == 1):
                 lo, hi, _ = key.indices(self.size)
                 hi = max(lo, hi)
-                return PaillierArray.from_buffers(self.context, self._w[lo:hi], self._e[lo:hi], (hi - lo,))
+                return self._view(lo, self._e[lo:hi], (hi - lo,))
         if isinstance(key, tuple) and len(key) == self.ndim and all(isinstance(k, (int, np.integer)) for k in key):
             idx = np.ravel_multi_index(tuple(int(k) % s for k, s in zip(key, self._shape)), self._shape)
             return self._elem(int(idx))
@@ -179,9 +240,10 @@ class PaillierArray:
             raise TypeError(f"can only assign PaillierCiphertext values, got {type(value)}")
         if not _same_key(src.context, self.context):
             raise ValueError("Adding two ciphertext with different keys.")
-        src = src._aligned_words(self._w.shape[1])
+        src = src._aligned_words(self._st.n2w)
         ib = np.broadcast_to(src._index_map(), sel.shape).reshape(-1)
-        self._w[sel.reshape(-1)] = src._w[ib]
+        self._st.host()[self._lo + sel.reshape(-1)] = src._w[ib]
+        self._st.host_written()
         self._e[sel.reshape(-1)] = src._e[ib]
 
     def __iter__(self):
@@ -201,7 +263,7 @@ class PaillierArray:
         if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
             shape = tuple(shape[0])
         new = np.empty(self._shape, dtype=np.bool_).reshape(shape).shape  # numpy's -1 / size rules
-        return PaillierArray.from_buffers(self.context, self._w, self._e, new)
+        return self._view(0, self._e, new)
 
     def flatten(self, order="C"):
         return self.reshape(-1).copy() if order in ("C", "A") else self.transpose().reshape(-1)
@@ -219,7 +281,30 @@ class PaillierArray:
         return self.reshape(np.empty(self._shape, dtype=np.bool_).squeeze(axis).shape)
 
     def copy(self, order="C"):
+        if self._st.d is not None:
+            d = self._st.d if self._whole() else self._st.d[self._lo:self._lo + self.size]
+            return PaillierArray.from_device(self.context, resident.clone(d), self._e.copy(), self._shape)
         return PaillierArray.from_buffers(self.context, self._w.copy(), self._e.copy(), self._shape)
+
+    def _obfuscate_in_place(self):
+        """Paillier.obfuscate on the array (paillier.py:419-431): every
+        element re-randomised in place, views included"""
+        ctx = self.context
+        n2w = ops.n2w_of(ctx)
+        if self._st.n2w != n2w:
+            raise ValueError(f"ciphertext rows of {self._st.n2w} words, the key's n^2 has {n2w}")
+        dev = resident.device_for(ctx)
+        if self._resident_on(dev):
+            new = resident.obfuscate(ctx.device_key(dev), self._dw(dev))
+            if self._whole():
+                self._st.d = new
+            else:
+                resident.put_rows(self._st.d, np.arange(self._lo, self._lo + self.size), new)
+            self._st.h = None  # the host copy is stale
+            return
+        h = self._st.host()
+        h[self._lo:self._lo + self.size] = ops.obfuscate_words(ctx, h[self._lo:self._lo + self.size])
+        self._st.host_written()
 
     def tolist(self):
         return self._objects().tolist()
@@ -249,7 +334,7 @@ class PaillierArray:
     def _aligned_words(self, n2w):
         """self with n2w-word rows (arrays decoded without a context keep the
         wire's width)."""
-        if self._w.shape[1] == n2w:
+        if self._st.n2w == n2w:
             return self
         if self._w.shape[1] > n2w:
             if self._w[:, n2w:].any():
@@ -413,20 +498,50 @@ def _dispatch(fn, a, b, ufunc):
 
 
 def _bcast(a, b):
-    """broadcast flat index maps of two operands -> (ia, ib, shape)"""
+    """broadcast flat index maps of two operands -> (ia, ib, shape); an
+    operand whose shape is the result's gets None (the identity map)"""
     sa = a.shape if hasattr(a, "shape") else ()
     sb = b.shape if hasattr(b, "shape") else ()
     shape = np.broadcast_shapes(sa, sb)
-    ia = np.broadcast_to(np.arange(int(np.prod(sa, dtype=np.int64)), dtype=np.int64).reshape(sa), shape).reshape(-1)
-    ib = np.broadcast_to(np.arange(int(np.prod(sb, dtype=np.int64)), dtype=np.int64).reshape(sb), shape).reshape(-1)
-    return ia, ib, shape
+
+    def imap(s):
+        if tuple(s) == tuple(shape):
+            return None
+        return np.broadcast_to(np.arange(int(np.prod(s, dtype=np.int64)), dtype=np.int64).reshape(s), shape).reshape(-1)
+    return imap(sa), imap(sb), shape
+
+
+def _identity(idx, size):
+    return idx is None or (idx.shape[0] == size and (size == 0 or (idx[0] == 0 and np.all(np.diff(idx) == 1))))
+
+
+def _at(flat, idx):
+    return flat if idx is None else flat[idx]
 
 
 def _rows(x, idx):
     """rows of x at idx, without a copy when idx is the identity"""
-    if idx.shape[0] == x.size and (x.size == 0 or (idx[0] == 0 and np.all(np.diff(idx) == 1))):
+    if _identity(idx, x.size):
         return x._w, x._e
     return x._w[idx], x._e[idx]
+
+
+def _drows(x, idx, dev):
+    """_rows on device words (resident.py)"""
+    d = x._dw(dev)
+    if _identity(idx, x.size):
+        return d, x._e
+    return resident.take(d, idx), x._e[idx]
+
+
+def _res_dev(ctx, *xs):
+    """The GPU to run a batched op on in HBM: the context's own GPU when some
+    ciphertext operand is resident there (results then stay there); None ->
+    the host-buffer path (xfl_amd.paillier.ops)."""
+    dev = resident.device_for(ctx)
+    if dev is not None and any(x is not None and x._resident_on(dev) for x in xs):
+        return dev
+    return None
 
 
 def _ctx_of(*xs):
@@ -463,10 +578,7 @@ def _add(a, b):
         n2w = ops.n2w_of(ctx)
         ca, cb = ca._aligned_words(n2w), cb._aligned_words(n2w)
         ia, ib, shape = _bcast(ca, cb)
-        wa, ea = _rows(ca, ia)
-        wb, eb = _rows(cb, ib)
-        w, e = ops.add_words(ctx, wa, ea, wb, eb)
-        return _result(ctx, w, e, shape)
+        return _add_rows(ctx, ca, ia, cb, ib, shape)
     if ca is None and cb is not None:
         a, b, ca, cb = b, a, cb, ca
     if ca is None:
@@ -479,10 +591,34 @@ def _add(a, b):
     ctx = _ctx_of(ca)
     ca = ca._aligned_words(ops.n2w_of(ctx))
     ia, ib, shape = _bcast(ca, p)
-    enc = _encrypt_plain(ctx, np.asarray(p).reshape(-1)[ib] if p.ndim else np.repeat(np.asarray(p).reshape(1), ib.size))
-    wa, ea = _rows(ca, ia)
-    w, e = ops.add_words(ctx, wa, ea, enc._w, enc._e)
-    return _result(ctx, w, e, shape)
+    nout = int(np.prod(shape, dtype=np.int64))
+    enc = _encrypt_plain(ctx, _at(np.asarray(p).reshape(-1), ib) if p.ndim else np.repeat(np.asarray(p).reshape(1), nout))
+    return _add_rows(ctx, ca, ia, enc, None, shape)
+
+
+def _add_rows(ctx, ca, ia, cb, ib, shape):
+    """ca[ia] + cb[ib] element-wise (paillier.py:106-123): in HBM when an
+    operand is resident there, else through host buffers"""
+    dev = _res_dev(ctx, ca, cb)
+    if dev is None:
+        wa, ea = _rows(ca, ia)
+        wb, eb = _rows(cb, ib)
+        w, e = ops.add_words(ctx, wa, ea, wb, eb)
+        return _result(ctx, w, e, shape)
+    da, ea = _drows(ca, ia, dev)
+    db, eb = _drows(cb, ib, dev)
+    n = ea.shape[0]
+    if n == 0:
+        return _result(ctx, np.zeros((0, ops.n2w_of(ctx)), np.uint32), np.zeros(0, np.int32), shape)
+    lo, hi = min(int(ea.min()), int(eb.min())), max(int(ea.max()), int(eb.max()))
+    dk = ctx.device_key(dev)
+    if lo == hi:  # one exponent throughout (the usual case): no alignment, nothing to upload
+        return PaillierArray.from_device(ctx, resident.mulmod(dk, da, None, db, None, 0), np.full(n, lo, np.int32),
+                                         shape)
+    wide = np.int32 if hi - lo < (1 << 31) else np.int64
+    dmax = int(np.max(np.abs(ea.astype(wide) - eb.astype(wide))))
+    out = resident.mulmod(dk, da, ea, db, eb, dmax)
+    return PaillierArray.from_device(ctx, out, np.minimum(ea, eb), shape)
 
 
 def _neg_plain(p):
@@ -575,8 +711,16 @@ def _mul(a, b):
     ctx = _ctx_of(ca)
     ca = ca._aligned_words(ops.n2w_of(ctx))
     ia, ib, shape = _bcast(ca, p)
-    P = np.asarray(p).reshape(-1)[ib] if np.ndim(p) else np.repeat(np.asarray(p).reshape(1), ib.size)
+    nout = int(np.prod(shape, dtype=np.int64))
+    P = _at(np.asarray(p).reshape(-1), ib) if np.ndim(p) else np.repeat(np.asarray(p).reshape(1), nout)
     kabs, neg, ek = _encode_scalars(ctx, P)
+    dev = _res_dev(ctx, ca)
+    if dev is not None:
+        da, ea = _drows(ca, ia, dev)
+        e = (ea.astype(np.int64) + ek).astype(np.int32)
+        if e.shape[0] == 0:
+            return _result(ctx, np.zeros((0, ops.n2w_of(ctx)), np.uint32), e, shape)
+        return PaillierArray.from_device(ctx, ops.raw_mul_dev(ctx.device_key(dev), da, kabs, neg), e, shape)
     wa, ea = _rows(ca, ia)
     w = ops.raw_mul_words(ctx, wa, kabs, neg)
     e = (ea.astype(np.int64) + ek).astype(np.int32)
@@ -616,16 +760,23 @@ def _sum(x, axis=None, keepdims=False):
     seglen = x.size // nseg if nseg else 0
     if seglen == 0:
         raise _Fallback()  # empty reduction: the reference's object sum gives int 0
-    order = perm.reshape(-1)
-    w, e = _rows(x, order)
+    order = None if keep + list(axes) == list(range(x.ndim)) else perm.reshape(-1)
     seg = np.arange(nseg + 1, dtype=np.int64) * seglen
+    dev = _res_dev(ctx, x)
     # numpy's add.reduce over an object array is a left fold in this order
-    rw, re = ops.segment_sums_words(ctx, w, e, seg, fold=True)
+    if dev is not None:
+        dw, e = _drows(x, order, dev)
+        rd, re = ops.segment_sums_dev(ctx, ctx.device_key(dev), dw, e, seg, fold=True)
+        res = lambda shp: PaillierArray.from_device(ctx, rd, re, shp)  # noqa: E731
+    else:
+        w, e = _rows(x, order)
+        rw, re = ops.segment_sums_words(ctx, w, e, seg, fold=True)
+        res = lambda shp: _result(ctx, rw, re, shp)  # noqa: E731
     if keepdims:
         out_shape = tuple(1 if d in axes else x.shape[d] for d in range(x.ndim))
     if not out_shape:
-        return _result(ctx, rw, re, (1,))._elem(0)
-    return _result(ctx, rw, re, out_shape)
+        return res((1,))._elem(0)
+    return res(out_shape)
 
 
 def _f_sum(a, axis=None, dtype=None, out=None, keepdims=False, initial=None, where=None):
@@ -652,9 +803,14 @@ def _f_concatenate(arrays, axis=0, out=None, dtype=None, casting="same_kind"):
         idx_parts.append(c._index_map() + off)
         off += c.size
     idx = np.concatenate(idx_parts, axis=axis)
-    w = np.concatenate([c._w for c in cs]) if cs else np.zeros((0, n2w), np.uint32)
     e = np.concatenate([c._e for c in cs])
     flat = idx.reshape(-1)
+    dev = _res_dev(ctx, *cs)
+    if dev is not None:
+        d = resident.cat([c._dw(dev) for c in cs])
+        return PaillierArray.from_device(ctx, d if _identity(flat, d.shape[0]) else resident.take(d, flat), e[flat],
+                                         idx.shape)
+    w = np.concatenate([c._w for c in cs]) if cs else np.zeros((0, n2w), np.uint32)
     return _result(ctx, w[flat], e[flat], idx.shape)
 
 
@@ -729,29 +885,67 @@ def _matvec(A, X):
     Bn, D = X.shape
     cexp = A._e.astype(np.int64)
     kw_, neg, e_k = _encode_scalars(ctx, np.asarray(X))
-    if kw_.ndim == 1:  # int64 |k| from the vectorised encoder
-        kw_ = np.ascontiguousarray(kw_, dtype=np.uint64).view(np.uint32).reshape(-1, 2)
-    ks = nat.words_to_ints(kw_)  # |k_ij|, row-major [B, D]
+    kvec = kw_.ndim == 1  # int64 |k| from the vectorised encoder
+    ks = None if kvec else nat.words_to_ints(kw_)  # |k_ij|, row-major [B, D]
     neg = neg.reshape(Bn, D)
     ex = cexp[:, None] + e_k.reshape(Bn, D)
     emin = ex.min(axis=0)
     need_inv = np.nonzero(neg.any(axis=1))[0]
-    bases = A._w
+    dev = _res_dev(ctx, A)
     inv_slot = np.full(Bn, -1, dtype=np.int64)
-    if need_inv.size:
-        one = np.zeros((need_inv.size, 1), dtype=np.uint32)
-        one[:, 0] = 1
-        inv = ops.powmod_words(ctx, A._w[need_inv], one, 1, invert_first=True)
-        inv_slot[need_inv] = Bn + np.arange(need_inv.size)
-        bases = np.concatenate([A._w, inv])
+    if dev is not None:
+        dk = ctx.device_key(dev)
+        bases = A._dw(dev)
+        if need_inv.size:
+            inv = resident.invert(dk, resident.take(bases, need_inv))
+            inv_slot[need_inv] = Bn + np.arange(need_inv.size)
+            bases = resident.cat([bases, inv])
+    else:
+        bases = A._w
+        if need_inv.size:
+            one = np.zeros((need_inv.size, 1), dtype=np.uint32)
+            one[:, 0] = 1
+            inv = ops.powmod_words(ctx, A._w[need_inv], one, 1, invert_first=True)
+            inv_slot[need_inv] = Bn + np.arange(need_inv.size)
+            bases = np.concatenate([A._w, inv])
     rows = np.arange(Bn, dtype=np.int64)
     idx = np.where(neg, inv_slot[:, None], rows[:, None]).T.astype(np.int32)  # [D, B]
     shift = (ex - emin[None, :]).T  # [D, B]
-    exps = [ks[i * D + j] << int(shift[j, i]) for j in range(D) for i in range(Bn)]
-    kbits = max(1, max(k.bit_length() for k in exps))
-    kw = (kbits + 31) // 32
-    r = ops.multiexp_words(ctx, bases, idx, nat.ints_to_words(exps, kw), kbits)
+    if kvec:
+        kwords, kbits = _shifted_words(np.ascontiguousarray(kw_.reshape(Bn, D).T), shift)
+    else:
+        exps = [ks[i * D + j] << int(shift[j, i]) for j in range(D) for i in range(Bn)]
+        kbits = max(1, max(k.bit_length() for k in exps))
+        kwords = nat.ints_to_words(exps, (kbits + 31) // 32)
+    if dev is not None:
+        r = resident.multiexp(dk, bases, idx, kwords, kbits)
+        return PaillierArray.from_device(ctx, r, emin.astype(np.int32), (D,))
+    r = ops.multiexp_words(ctx, bases, idx, kwords, kbits)
     return _result(ctx, r, emin.astype(np.int32), (D,))
+
+
+def _shifted_words(k, shift):
+    """words of k << shift for int64 k >= 0 (< 2^63) and shifts >= 0, same
+    shape -> (uint32 [k.size, kw], kbits) with every value < 2^kbits: the
+    aligned multi-exponentiation exponents without a Python int per term"""
+    k = k.reshape(-1).astype(np.uint64)
+    s = shift.reshape(-1).astype(np.int64)
+    nz = k != 0
+    if not nz.any():
+        return np.zeros((k.size, 1), np.uint32), 1
+    kb = np.frexp(k[nz].astype(np.float64))[1].astype(np.int64)  # >= the bit length (float rounding up)
+    kbits = int((kb + s[nz]).max())
+    kw = (kbits + 31) // 32
+    out = np.zeros((k.size, kw + 3), np.uint32)
+    w0 = np.where(nz, s // 32, 0)  # zero terms may carry any shift
+    b = (s % 32).astype(np.uint64)
+    lo = k << b  # < 2^94 in all: three words from word w0 (numpy's uint64 shift wraps)
+    hi = np.where(b > 0, k >> (np.uint64(64) - np.where(b > 0, b, np.uint64(1))), np.uint64(0))
+    r = np.arange(k.size)
+    out[r, w0] = (lo & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    out[r, w0 + 1] = (lo >> np.uint64(32)).astype(np.uint32)
+    out[r, w0 + 2] = hi.astype(np.uint32)
+    return np.ascontiguousarray(out[:, :kw]), kbits
 
 
 _UFUNCS = {np.add: _add, np.subtract: _sub, np.multiply: _mul, np.true_divide: _div, np.matmul: _matmul,

@@ -220,13 +220,7 @@ def raw_mul_words(ctx, cw, kabs, neg, num_cores=-1):
     out = np.empty_like(cw)
     if n == 0:
         return out
-    if isinstance(kabs, np.ndarray) and kabs.ndim == 1:
-        kabs = np.ascontiguousarray(kabs, dtype=np.uint64)
-        kw_ = kabs.view(np.uint32).reshape(n, 2)
-        kbits = max(1, int(kabs.max()).bit_length())
-    else:
-        kw_ = _u32(kabs)
-        kbits = max(1, max(nat.words_to_ints(kw_)).bit_length()) if n else 1
+    kw_, kbits = _scalar_words(kabs, n)
     neg = np.asarray(neg, dtype=bool).reshape(-1)
     for flag in (False, True):
         idx = np.nonzero(neg == flag)[0]
@@ -236,6 +230,31 @@ def raw_mul_words(ctx, cw, kabs, neg, num_cores=-1):
             out[:] = powmod_words(ctx, cw, kw_, kbits, flag, num_cores)
         else:
             out[idx] = powmod_words(ctx, cw[idx], kw_[idx], kbits, flag, num_cores)
+    return out
+
+
+def _scalar_words(kabs, n):
+    """|k| (int64 array or [n, kw] uint32 words) -> (words, bit length)"""
+    if isinstance(kabs, np.ndarray) and kabs.ndim == 1:
+        kabs = np.ascontiguousarray(kabs, dtype=np.uint64)
+        return kabs.view(np.uint32).reshape(n, 2), max(1, int(kabs.max()).bit_length())
+    kw_ = _u32(kabs)
+    return kw_, (max(1, max(nat.words_to_ints(kw_)).bit_length()) if n else 1)
+
+
+def raw_mul_dev(dk, d, kabs, neg):
+    """raw_mul_words on device words (resident.py): c^|k|, or inv(c)^|k| for
+    the negative branch, per element -> device words"""
+    from . import resident
+    n = d.shape[0]
+    kw_, kbits = _scalar_words(kabs, n)
+    neg = np.asarray(neg, dtype=bool).reshape(-1)
+    if not neg.any() or neg.all():
+        return resident.powmod(dk, d, kw_, kbits, bool(neg[0]))
+    out = resident.empty(dk.device, tuple(d.shape))
+    for flag in (False, True):
+        idx = np.nonzero(neg == flag)[0]
+        resident.put_rows(out, idx, resident.powmod(dk, resident.take(d, idx), kw_[idx], kbits, flag))
     return out
 
 
@@ -311,10 +330,20 @@ def segment_sums_words(ctx, cw, exps, seg_begin, gap_powers=None, fold=False):
     leaves' final powers, or fold=True derives them for left folds of each
     segment in input order (fold_gap_powers); such leaves are raised to their
     power first and enter the product unaligned."""
+    cw = _u32(cw)
+    seg, emin, d, gap_powers = _segment_plan(ctx, cw.shape[0], exps, seg_begin, gap_powers, fold)
+    if gap_powers:
+        idx = np.fromiter(gap_powers.keys(), dtype=np.int64, count=len(gap_powers))
+        cw = cw.copy()
+        cw[idx] = pow_signed_words(ctx, cw[idx], [gap_powers[int(i)] for i in idx])
+        d[idx] = 0
+    return segprod_words(ctx, cw, d, seg), emin.astype(np.int32)
+
+
+def _segment_plan(ctx, n, exps, seg_begin, gap_powers, fold):
+    """(offsets, per-segment min exponent, per-element shift d, gap powers)"""
     seg = np.ascontiguousarray(seg_begin, dtype=np.int64)
     nseg = seg.shape[0] - 1
-    cw = _u32(cw)
-    n = cw.shape[0]
     e = np.asarray(exps, dtype=np.int64).reshape(-1)
     lens = np.diff(seg)
     emin = np.zeros(nseg, dtype=np.int64)
@@ -324,12 +353,23 @@ def segment_sums_words(ctx, cw, exps, seg_begin, gap_powers=None, fold=False):
     d = (e - np.repeat(emin, lens)).astype(np.int32)
     if fold and n and gap_powers is None:
         gap_powers = fold_gap_powers(ctx, e, seg)
+    return seg, emin, d, gap_powers
+
+
+def segment_sums_dev(ctx, dk, cd, exps, seg_begin, gap_powers=None, fold=False):
+    """segment_sums_words on device words -> (device [nseg, n2w], emin)"""
+    from . import resident
+    seg, emin, d, gap_powers = _segment_plan(ctx, cd.shape[0], exps, seg_begin, gap_powers, fold)
     if gap_powers:
         idx = np.fromiter(gap_powers.keys(), dtype=np.int64, count=len(gap_powers))
-        cw = cw.copy()
-        cw[idx] = pow_signed_words(ctx, cw[idx], [gap_powers[int(i)] for i in idx])
+        powers = [gap_powers[int(i)] for i in idx]
+        kabs = [abs(int(E)) for E in powers]
+        kw = max(1, (max(k.bit_length() for k in kabs) + 31) // 32)
+        cd = resident.clone(cd)
+        resident.put_rows(cd, idx, raw_mul_dev(dk, resident.take(cd, idx), nat.ints_to_words(kabs, kw),
+                                               np.array([E < 0 for E in powers], dtype=bool)))
         d[idx] = 0
-    return segprod_words(ctx, cw, d, seg), emin.astype(np.int32)
+    return resident.segprod(dk, cd, d, seg), emin.astype(np.int32)
 
 
 def segprod_words(ctx, cw, d, seg):

@@ -11,7 +11,7 @@ from typing import Optional, Union
 import numpy as np
 
 from .. import _native as nat
-from . import ops
+from . import ops, resident
 from .context import PaillierContext
 from .encoder import PaillierEncoder, int_to_float_gmpy
 from .utils import MPZ, get_core_num  # noqa: F401  (re-exported like the reference)
@@ -277,7 +277,15 @@ class Paillier(object):
             shape = data.shape
             flat = data.reshape(-1)
             n = flat.shape[0]
+            dev = resident.device_for(context, num_cores) if n else None
             if flat.dtype.kind == "f":
+                if dev is not None:  # results stay in HBM (resident.py)
+                    if obfuscation:
+                        context.note_encrypt_volume(n)
+                    d, e, st = resident.encrypt_floats(context.device_key(dev), flat, precision, max_exponent,
+                                                       obfuscation)
+                    Paillier._raise_status(st)
+                    return PaillierArray.from_device(context, d, e, shape)
                 w, e, st = ops.encrypt_floats_words(context, flat, precision, max_exponent, obfuscation, num_cores)
                 Paillier._raise_status(st)
                 return PaillierArray.from_buffers(context, w, e, shape)
@@ -287,6 +295,12 @@ class Paillier(object):
             fl_idx, int_idx = [], []
             if flat.dtype.kind in "iub":
                 int_idx = range(n)
+                if dev is not None:
+                    ms, es = _encode_ints(context, flat.tolist(), precision, max_exponent)
+                    if obfuscation:
+                        context.note_encrypt_volume(n)
+                    d = resident.encrypt_encoded(context.device_key(dev), nat.ints_to_words(ms, nw), obfuscation)
+                    return PaillierArray.from_device(context, d, np.asarray(es, dtype=np.int32), shape)
             else:
                 for i, x in enumerate(flat):
                     if isinstance(x, (float, np.floating)):
@@ -346,6 +360,19 @@ class Paillier(object):
             raise TypeError("Try to decrypt a paillier ciphertext by a public key.")
         if isinstance(data, PaillierArray):
             arr = data._aligned_words(ops.n2w_of(context))
+            dev = resident.device_for(context, num_cores)
+            if arr.size and arr._resident_on(dev):  # in HBM: only the results come back
+                dk = context.device_key(dev)
+                if not out_origin and dtype == 'float':
+                    _, f32, st = resident.decrypt_decode(dk, arr._dw(dev), arr.exponents)
+                    if np.any(st != 0):
+                        raise OverflowError("Overflow detected during decoding encrypted number.")
+                    return f32.reshape(arr.shape)
+                ms = nat.words_to_ints(resident.decrypt(dk, arr._dw(dev)))
+                vals = [PaillierEncoder.decode_single(context, m, int(e)) for m, e in zip(ms, arr.exponents.tolist())]
+                out = np.empty(len(vals), dtype=object)
+                out[:] = vals
+                return _finish_decrypt(out.reshape(arr.shape), dtype, out_origin)
             if not out_origin and dtype == 'float':
                 # decrypt + decode + float32 on the device, straight from the words
                 _, f32, st = ops.decrypt_decode_words(context, arr.words, arr.exponents, num_cores)
@@ -398,7 +425,7 @@ class Paillier(object):
             if ciphertext.size:
                 if ctx is None:
                     raise ValueError("ciphertext array without a context")
-                ciphertext.words[:] = ops.obfuscate_words(ctx, ciphertext._aligned_words(ops.n2w_of(ctx)).words)
+                ciphertext._obfuscate_in_place()
             return ciphertext
         if isinstance(ciphertext, np.ndarray):
             flat = ciphertext.reshape(-1)
