@@ -120,8 +120,12 @@ def test_djn_encrypt_both_shapes():
             big = words_to_ints(dk.encrypt_words(mw, rw))
             small = words_to_ints(dk.encrypt_words(mw[:SMALL], rw[:SMALL]))
             assert small == big[:SMALL]
+            # 2048 bits (Montgomery-digit kernel): 16 lanes per element up to
+            # 2 k elements, 4 up to 16 k, 1 beyond - three splits of the windows
+            mid = words_to_ints(dk.encrypt_words(mw[:3000], rw[:3000]))
+            assert mid == big[:3000]
             ok = O.derive_private(p, q, h)
-            for i in (0, SMALL - 1, nbig - 1):
+            for i in (0, SMALL - 1, 2999, nbig - 1):
                 assert big[i] == O.encrypt_m(ok, ms[i], rs[i])
 
 

@@ -306,6 +306,45 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o_nR2n2 = bl.put_limbs(mulmod(n, mulmod(Rn2, Rn2, n2), n2), k->mn2);
     if (h && !p) o_hMn2 = bl.put_limbs(mulmod(mod(*h, n2), Rn2, n2), k->mn2);  // public DJN table base
   }
+#if XHE_NDIG
+  // Montgomery digits mod n^2 (PMDX<80, 4>, pdigit_dev.hpp): n in 80 limbs of
+  // 27 bits, R = 2^2160; ceil(R/n) n^2 (the input conversion's offset), R - n,
+  // the digits (e, f) of R^2 mod n^2 and of 1 (R e + n f = X R^2 mod n^2),
+  // MASK + E_i with E = (1 - R) mod n
+  struct {
+    ModOff nd;
+    size_t kn2 = 0, rmn = 0, dw = 0, d1 = 0, topc = 0;
+  } on;
+  if (K == 2048) {
+    const ModSpec sn{80, 27};
+    on.nd = put_mod(bl, n, sn);
+    const BigU R = pow2((size_t)27 * 80);
+    BigU q;
+    divmod(sub(add(R, n), BigU(1)), n, &q, nullptr);  // ceil(R / n)
+    on.kn2 = bl.put_limbs(mul(q, n2), ModSpec{160, 27});
+    on.rmn = bl.put_limbs(sub(R, n), sn);
+    const BigU Rn = mod(R, n), Rinv = modinv(Rn, n);
+    auto digits = [&](const BigU& X) {
+      const BigU e = mulmod(mod(X, n), Rinv, n);
+      BigU Q;
+      divmod(add(X, mul(R, sub(n, e))), n, &Q, nullptr);  // (X - R e) / n + R
+      const BigU f = submod(mod(Q, n), Rn, n);
+      const std::vector<uint32_t> el = e.to_limbs(27, 80), fl = f.to_limbs(27, 80);
+      std::vector<uint32_t> v(160);
+      for (int i = 0; i < 80; ++i) {
+        v[2 * i] = el[i];
+        v[2 * i + 1] = fl[i];
+      }
+      return bl.put(v);
+    };
+    const BigU R2 = mulmod(mod(R, n2), mod(R, n2), n2);  // R^2 mod n^2
+    on.d1 = digits(R2);                                   // 1 R^2
+    on.dw = digits(mulmod(R2, R2, n2));                   // R^2 R^2
+    std::vector<uint32_t> tc = submod(BigU(1), Rn, n).to_limbs(27, 80);
+    for (auto& x : tc) x += (1u << 27) - 1u;
+    on.topc = bl.put(tc);
+  }
+#endif
   // randomness bound (paillier.py:195 djn_exp_bound = 2^(bitlen(n)//2); :215 r < n)
   k->rand_bits = k->djn ? (int)(n.bits() / 2) : (int)n.bits();
   k->rand_words = (k->rand_bits + 31) / 32;
@@ -435,6 +474,17 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   kd.n2X = moddev(B, o_n2X);
   kd.nR2_n2 = B + o_nR2n2;
   kd.n_bits = (int)n.bits();
+#if XHE_NDIG
+  if (K == 2048) {
+    kd.ndig = 1;
+    kd.nd = moddev(B, on.nd);
+    kd.nd_kn2 = B + on.kn2;
+    kd.nd_rmn = B + on.rmn;
+    kd.nd_topc = B + on.topc;
+    kd.nd_dw = reinterpret_cast<const uint2*>(B + on.dw);
+    kd.nd_d1 = reinterpret_cast<const uint2*>(B + on.d1);
+  }
+#endif
   if (k->priv) {
     kd.p2 = moddev(B, o.p2);
     kd.p2L = moddev(B, o.p2L);
@@ -650,6 +700,18 @@ void crt_enc_launch(const xhe_key* k, int64_t n, uint32_t* ws, uint32_t* ct, hip
   HIPCHK(hipGetLastError());
 }
 
+// lanes per element of k_djn_pmd: 16 up to 2 k elements, 4 up to 16 k, else
+// 1 (the chip holds ~128 k one-lane residues: 2 waves x 1024 SIMDs x 64);
+// $XHE_PMD_SPLIT pins it (1, 4 or 16)
+int pmd_split(int64_t n) {
+  static const int pin = [] {
+    const char* e = getenv("XHE_PMD_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (pin == 1 || pin == 4 || pin == 16) return pin;
+  return n <= 2048 ? 16 : n <= 16384 ? 4 : 1;
+}
+
 template <class Sh>
 void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -663,10 +725,17 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     if constexpr (Sh::K == 2048) {
       if (k->kd.pmd) {
         ProfScope ps("k_djn_pow", s);
-        const dim3 grid((unsigned)((n + 127) / 128), 2);
-        hipLaunchKernelGGL((k_djn_pmd<MP2, 37, Sh::RW>), grid, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N,
-                           k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
-                           k->rand_words, n, ws);
+        // small batches split each element's windows over G lanes (latency:
+        // ~nwin/G + log2 G dependent products instead of nwin)
+        const int G = pmd_split(n);
+        const dim3 grid((unsigned)((n * G + 127) / 128), 2);
+        auto launch = [&](auto kern) {
+          hipLaunchKernelGGL(kern, grid, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N, k->kd.q2.N,
+                             m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, ws);
+        };
+        if (G == 16) launch(k_djn_pmd<MP2, 37, Sh::RW, 16>);
+        else if (G == 4) launch(k_djn_pmd<MP2, 37, Sh::RW, 4>);
+        else launch(k_djn_pmd<MP2, 37, Sh::RW, 1>);
         HIPCHK(hipGetLastError());
         crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
         continue;
@@ -727,6 +796,45 @@ void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r
   ws_free(ws, s);
 }
 
+#if XHE_NDIG
+using ND2048 = PMDX<80, 4>;
+// $XHE_NDIG=0: the Montgomery mod-n^2 kernels instead (A/B measurement)
+bool ndig_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_NDIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// in -> exponentiation -> out over chunks of up to kChunk elements; the
+// exponentiation runs grid-stride over at most 1024 blocks (32 element groups
+// each, one digit table per group slot)
+template <class IN, class POW, class OUT>
+void ndig_run(int64_t count, hipStream_t s, IN&& in, POW&& pw, OUT&& out) {
+  using D = ND2048;
+  const int64_t chunk = std::min<int64_t>(count, kChunk);
+  const int pblocks = (int)std::min<int64_t>((chunk + NdigWs<D>::GPB - 1) / NdigWs<D>::GPB, 1024);
+  uint2 *st = nullptr, *tab = nullptr;
+  uint32_t* rows = nullptr;
+  ws_alloc((void**)&st, (size_t)D::K * chunk * sizeof(uint2), s);
+  ws_alloc((void**)&tab, NdigWs<D>::tab_bytes_per_slot() * (size_t)pblocks * NdigWs<D>::GPB, s);
+  ws_alloc((void**)&rows, (size_t)2 * D::MN::S4 * chunk * sizeof(uint32_t), s);
+  for (int64_t off = 0; off < count; off += chunk) {
+    const int64_t n = std::min(chunk, count - off);
+    const int eblocks = (int)((n * D::TPI + 127) / 128);
+    in(eblocks, off, n, st);
+    HIPCHK(hipGetLastError());
+    pw(std::min<int>(pblocks, (int)((n + NdigWs<D>::GPB - 1) / NdigWs<D>::GPB)), off, n, st, tab);
+    HIPCHK(hipGetLastError());
+    out(eblocks, off, n, st, rows);
+    HIPCHK(hipGetLastError());
+  }
+  ws_free(st, s);
+  ws_free(tab, s);
+  ws_free(rows, s);
+}
+#endif
+
 template <class Sh>
 void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
                         hipStream_t s) {
@@ -757,6 +865,27 @@ void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, 
     ws_free(ws, s);
     ws_free(rows, s);
   } else {
+#if XHE_NDIG
+    if constexpr (Sh::K == 2048) {
+      if (k->kd.ndig && ndig_on()) {
+        ndig_run(
+            count, s,
+            [&](int b, int64_t off, int64_t n, uint2* st) {
+              hipLaunchKernelGGL((k_ndig_in<ND2048, false>), dim3(b), dim3(128), 0, s, k->kd,
+                                 r + (size_t)off * k->rand_words, k->rand_words, n, st);
+            },
+            [&](int b, int64_t, int64_t n, uint2* st, uint2* tab) {
+              ProfScope ps("k_nodjn_pub", s);
+              hipLaunchKernelGGL(k_ndig_pow_n<ND2048>, dim3(b), dim3(128), 0, s, k->kd, n, st, tab);
+            },
+            [&](int b, int64_t off, int64_t n, uint2* st, uint32_t* rows) {
+              hipLaunchKernelGGL((k_ndig_out<ND2048, true>), dim3(b), dim3(128), 0, s, k->kd, st,
+                                 m + (size_t)off * k->nw, n, ct + (size_t)off * k->n2w, rows);
+            });
+        return;
+      }
+    }
+#endif
     using MN2 = typename Sh::MN2;
     int64_t chunk = std::min<int64_t>(count, kChunk);
     int pb = pow_grid<MN2>(chunk, 512);
@@ -815,6 +944,28 @@ void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const u
 template <class Sh, class MN2 = typename Sh::MN2>
 void powmod_impl(const xhe_key* k, const uint32_t* c, const uint32_t* kw_, int kw, int kbits, int64_t count,
                  uint32_t* out, hipStream_t s) {
+#if XHE_NDIG
+  if constexpr (Sh::K == 2048 && MN2::TPI == 4) {
+    if (k->kd.ndig && ndig_on()) {
+      ndig_run(
+          count, s,
+          [&](int b, int64_t off, int64_t n, uint2* st) {
+            hipLaunchKernelGGL((k_ndig_in<ND2048, true>), dim3(b), dim3(128), 0, s, k->kd, c + (size_t)off * k->n2w,
+                               k->n2w, n, st);
+          },
+          [&](int b, int64_t off, int64_t n, uint2* st, uint2* tab) {
+            ProfScope ps("k_powmod_n2", s);
+            hipLaunchKernelGGL(k_ndig_pow_k<ND2048>, dim3(b), dim3(128), 0, s, k->kd, kw_ + (size_t)off * kw, kw,
+                               kbits, n, st, tab);
+          },
+          [&](int b, int64_t off, int64_t n, uint2* st, uint32_t* rows) {
+            hipLaunchKernelGGL((k_ndig_out<ND2048, false>), dim3(b), dim3(128), 0, s, k->kd, st, nullptr, n,
+                               out + (size_t)off * k->n2w, rows);
+          });
+      return;
+    }
+  }
+#endif
   int64_t chunk = std::min<int64_t>(count, kChunk);
   int pb = pow_grid<MN2>(chunk, 512);
   int64_t groups = (int64_t)pb * 256 / MN2::TPI;

@@ -76,6 +76,13 @@ struct KeyDev {
   // tables hold digit pairs (pmd = 1); MASK + ((1 - R) mod P) limbs per prime
   int pmd;
   const uint32_t *topc_p, *topc_q;
+  // ---- Montgomery digits mod n^2 (PMDX, 2048-bit keys, public or private):
+  // n as 80 limbs of 27 bits (R = 2^2160), ceil(R/n) n^2 (160 limbs), R - n,
+  // the digits of R^2 mod n^2 and of 1 (80 pairs each), MASK + E_i
+  int ndig;
+  ModDev nd;
+  const uint32_t *nd_kn2, *nd_rmn, *nd_topc;
+  const uint2 *nd_dw, *nd_d1;
 };
 
 // ============================================================== encode
@@ -600,7 +607,15 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
 // P^2, to_mont2) for the two Montgomery products that bring in (1 + n m) and
 // leave Montgomery form, exactly as in djn_prime_lds. Output rows as
 // k_djn_pow_lds (MP2 limbs, [prime][2 S4][count]) for k_crt_enc_w.
-template <class MP2, int KP, int RW>
+//
+// G > 1 (small batches, where the chip is not full and the chain of nwin
+// dependent products is the latency): G adjacent lanes share an element; lane
+// g multiplies windows g, g + G, g + 2G, ... and the G partial products are
+// combined by a tree through the lanes' LDS slots (log2 G levels, the writer's
+// state streamed as the reader's operand), so the chain is ~nwin/G + log2 G
+// products; lane 0 of the group finishes. Products of Montgomery-digit states
+// are digit states of the product, so the result is the same residue.
+template <class MP2, int KP, int RW, int G = 1>
 __global__ void __launch_bounds__(128, 2) k_djn_pmd(KeyDev key, const uint32_t* __restrict__ Pp,
                                                     const uint32_t* __restrict__ Pq, const uint32_t* __restrict__ Np2,
                                                     const uint32_t* __restrict__ Nq2,
@@ -616,8 +631,11 @@ __global__ void __launch_bounds__(128, 2) k_djn_pmd(KeyDev key, const uint32_t* 
   const uint32_t* tc = prime ? key.topc_q : key.topc_p;
   if (threadIdx.x < KP) topc[threadIdx.x] = tc[threadIdx.x];
   __syncthreads();
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= count) return;
+  static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "lane groups of a power of two, inside one wave");
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = t / G;
+  const int g = (int)(threadIdx.x & (G - 1));
+  if (e >= count) return;  // whole groups (G divides the wave)
   uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
   uint32_t* slot = img + (threadIdx.x & 63) * 4;
   const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
@@ -635,16 +653,38 @@ __global__ void __launch_bounds__(128, 2) k_djn_pmd(KeyDev key, const uint32_t* 
     unpack_pairs_lds<KP, RW>(slot);
   };
   uint32_t a[KP], c[KP];
-  stage(0);
+  if (G == 1 || g < key.nwin) {
+    stage(g);
 #pragma unroll
-  for (int q = 0; q < D::NQ; ++q) {
-    const uint4 v = *reinterpret_cast<const uint4*>(slot + q * 256);
-    if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
-    if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+    for (int q = 0; q < D::NQ; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(slot + q * 256);
+      if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+      if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+    }
   }
-  for (int w = 1; w < key.nwin; ++w) {
+  for (int w = g + G; w < key.nwin; w += G) {
     stage(w);
     M.mul(a, c, slot, topc);
+  }
+  if constexpr (G > 1) {
+    // tree over the group: at level s, lane g + s (g a multiple of 2s) parks
+    // its state in its slot and lane g multiplies it in
+#pragma unroll
+    for (int s = 1; s < G; s <<= 1) {
+      const bool writer = (g & (2 * s - 1)) == s && g < key.nwin;
+      const bool reader = (g & (2 * s - 1)) == 0 && g + s < key.nwin;
+      if (writer) {
+#pragma unroll
+        for (int q = 0; q < D::NQ; ++q)
+          *reinterpret_cast<uint4*>(slot + q * 256) =
+              make_uint4(2 * q < KP ? a[2 * q] : 0u, 2 * q < KP ? c[2 * q] : 0u, 2 * q + 1 < KP ? a[2 * q + 1] : 0u,
+                         2 * q + 1 < KP ? c[2 * q + 1] : 0u);
+      }
+      wave_sync_mem_();
+      if (reader) M.mul(a, c, slot + 4 * s, topc);
+      wave_sync_mem_();
+    }
+    if (g != 0) return;
   }
   {
     uint32_t x[2 * KP];
@@ -1548,6 +1588,161 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_pub(KeyDev key, const uint32_t
     store_packed(M, b, tab + 16 * rs, st, out + (size_t)e * key.n2w, key.n2w);
   }
 }
+
+#if XHE_NDIG
+// ---------------------------------------------------------------------------
+// Variable-base exponentiations mod n^2 in Montgomery digits (PMDX, 4 lanes
+// per element, 2048-bit keys): 4 K^2 mads per squaring and 5 K^2 per product
+// at K = 80 instead of 2 S^2 = 46 k at S = 152 (Mont<152, 27, 4>), and half
+// as many dependent steps per product. Three kernels, so that each has the
+// registers to itself (together they spill): k_ndig_in (plain residue ->
+// digits), the exponentiation (k_ndig_pow_n: the exponent n shared by every
+// element; k_ndig_pow_k: a per-element exponent), k_ndig_out (digits ->
+// plain words, optionally times (1 + n m)). The digit state between them:
+// st[pair i][count] uint2. Blocks of 128 threads = 32 element groups.
+template <class D>
+struct NdigWs {
+  static constexpr int GPB = 128 / D::TPI;
+  // the exponentiation kernels' per-group-slot table: 16 entries x K pairs
+  static constexpr size_t tab_bytes_per_slot() { return (size_t)16 * D::K * 8; }
+};
+
+template <class D>
+XHE_DEV void ndig_st_store(const uint32_t (&a)[D::L], const uint32_t (&c)[D::L], uint2* st, int64_t count, int64_t e) {
+  const int g = D::G::g();
+  uint2* p = pmdx_launder(st) + e;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) p[(size_t)(g * D::L + j) * count] = make_uint2(a[j], c[j]);
+}
+template <class D>
+XHE_DEV void ndig_st_load(uint32_t (&a)[D::L], uint32_t (&c)[D::L], const uint2* st, int64_t count, int64_t e) {
+  const int g = D::G::g();
+  const uint2* p = pmdx_launder(st) + e;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) {
+    const uint2 v = p[(size_t)(g * D::L + j) * count];
+    a[j] = v.x;
+    c[j] = v.y;
+  }
+}
+
+// x (WIDE: n2w ciphertext words, else nwords words of a value < n) -> digits
+template <class D, bool WIDE>
+__global__ void __launch_bounds__(128, 2) k_ndig_in(KeyDev key, const uint32_t* __restrict__ x, int nwords,
+                                                    int64_t count, uint2* __restrict__ st) {
+  constexpr int L = D::L;
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = key.nd_topc[i];
+  __syncthreads();
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  D X;
+  X.init(key.nd.N, key.nd.n0inv);
+  uint32_t lo[L], hi[L], a[L], c[L];
+  const uint32_t* xe = x + (size_t)e * nwords;
+  pmdx_load<D, 0>(lo, xe, nwords, g);
+  if constexpr (WIDE) {
+    pmdx_load<D, D::K>(hi, xe, nwords, g);
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) hi[j] = 0;
+  }
+  pmdx_to_digits(X, lo, hi, key.nd_kn2, key.nd_rmn, key.nd_dw, topc, a, c);
+  ndig_st_store<D>(a, c, st, count, e);
+}
+
+// st <- st^n (public non-DJN obfuscator r^n, paillier.py:228-230)
+template <class D>
+__global__ void __launch_bounds__(128, 2) k_ndig_pow_n(KeyDev key, int64_t count, uint2* __restrict__ st,
+                                                       uint2* __restrict__ ws) {
+  constexpr int GPB = NdigWs<D>::GPB, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = key.nd_topc[i];
+  __syncthreads();
+  const int gs = (int)gridDim.x * GPB;
+  const int gid0 = (int)blockIdx.x * GPB + (int)threadIdx.x / D::TPI;
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  uint2* tab = ws + gid0;
+  for (int64_t e = gid0; e < count; e += gs) {
+    D X;
+    X.init(key.nd.N, key.nd.n0inv);
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, st, count, e);
+    pmdx_pow_uniform(X, a, c, key.n_words, key.n_bits, tab, gs, ops, GPB, topc);
+    ndig_st_store<D>(a, c, st, count, e);
+  }
+}
+
+// st <- st^k, k per element (kw words, < 2^kbits): _raw_mul's positive
+// branch (paillier.py:156-187), 4-bit fixed windows
+template <class D>
+__global__ void __launch_bounds__(128, 2) k_ndig_pow_k(KeyDev key, const uint32_t* __restrict__ k, int kw, int kbits,
+                                                       int64_t count, uint2* __restrict__ st, uint2* __restrict__ ws) {
+  constexpr int GPB = NdigWs<D>::GPB, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = key.nd_topc[i];
+  __syncthreads();
+  const int gs = (int)gridDim.x * GPB;
+  const int gid0 = (int)blockIdx.x * GPB + (int)threadIdx.x / D::TPI;
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  uint2* tab = ws + gid0;
+  const int nwin = kbits <= 0 ? 1 : (kbits + 3) / 4;
+  for (int64_t e = gid0; e < count; e += gs) {
+    D X;
+    X.init(key.nd.N, key.nd.n0inv);
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, st, count, e);
+    const uint32_t* ke = k + (size_t)e * kw;
+    pmdx_pow_window4(X, a, c, nwin, [&](int w) { return nibble(ke, kw, w); }, key.nd_d1, tab, gs, ops, GPB, topc);
+    ndig_st_store<D>(a, c, st, count, e);
+  }
+}
+
+// digits -> ciphertext words y = y0 + n y1; FOLD: times (1 + n m), m words
+// per element (nw): y0 + n ((y1 + y0 m) mod n)   (paillier.py:228-230, 283)
+template <class D, bool FOLD>
+__global__ void __launch_bounds__(128, 2) k_ndig_out(KeyDev key, const uint2* __restrict__ st,
+                                                     const uint32_t* __restrict__ m_words, int64_t count,
+                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ ws) {
+  constexpr int L = D::L;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  D X;
+  X.init(key.nd.N, key.nd.n0inv);
+  uint32_t y0[L], y1[L];
+  {
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, st, count, e);
+    pmdx_from_digits(X, a, c, y0, y1);
+  }
+  uint32_t* rows = ws + e;  // 2 x S4 limb rows, stride count
+  const int cnt = (int)count;
+  if constexpr (FOLD) {
+    uint32_t* mrow = rows + (size_t)D::MN::S4 * count;
+    uint32_t z[L];
+    pmdx_load<D, 0>(z, m_words + (size_t)e * key.nw, key.nw, g);
+    X.M.store_strided(z, mrow, cnt);
+    wave_sync_mem_();
+#pragma unroll
+    for (int j = 0; j < L; ++j) z[j] = y0[j];
+    X.M.mul(z, AStrided{mrow, cnt});  // y0 m R^-1
+    X.M.mul(z, ARow{key.nd.R2});      // y0 m (< 2n)
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = (uint64_t)y1[j] + z[j];
+    D::normalize_top(T, y1);
+    X.M.reduce_once(y1);
+    X.M.reduce_once(y1);
+  }
+  X.M.store_strided(y0, rows, cnt);
+  wave_sync_mem_();
+  X.M.wide_mul_add_store(y1, ARow{key.nd.N}, rows, cnt, out + (size_t)e * key.n2w, key.n2w);
+}
+#endif
 
 // SHAPE 0: the batch shape (key.p2/q2); 1: the 4-lane shape (key.p2L/q2L),
 // for key sizes whose batch shape spills in this exponentiation (3072 bits:

@@ -534,12 +534,20 @@ def _drows(x, idx, dev):
     return resident.take(d, idx), x._e[idx]
 
 
+SMALL = 1 << 16  # host-only operands up to this many elements are uploaded (no host pipeline set-up)
+
+
 def _res_dev(ctx, *xs):
     """The GPU to run a batched op on in HBM: the context's own GPU when some
-    ciphertext operand is resident there (results then stay there); None ->
-    the host-buffer path (xfl_amd.paillier.ops)."""
+    ciphertext operand is resident there, or when the host-only operands are
+    small (uploading them costs less than the host pipeline's set-up); results
+    then stay in HBM. None -> the host-buffer path (xfl_amd.paillier.ops),
+    which overlaps the copies of large host arrays with the kernels."""
     dev = resident.device_for(ctx)
-    if dev is not None and any(x is not None and x._resident_on(dev) for x in xs):
+    if dev is None:
+        return None
+    xs = [x for x in xs if x is not None]
+    if any(x._resident_on(dev) for x in xs) or sum(x.size for x in xs) <= SMALL:
         return dev
     return None
 

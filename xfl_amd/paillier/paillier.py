@@ -355,13 +355,14 @@ class Paillier(object):
     def decrypt(cls, context: PaillierContext, data: Union[PaillierCiphertext, np.ndarray], dtype: str = 'float',
                 num_cores: int = -1, out_origin: bool = False):
         """paillier.py:370-417"""
-        from .array import PaillierArray
+        from .array import SMALL, PaillierArray
         if not context.is_private():
             raise TypeError("Try to decrypt a paillier ciphertext by a public key.")
         if isinstance(data, PaillierArray):
             arr = data._aligned_words(ops.n2w_of(context))
             dev = resident.device_for(context, num_cores)
-            if arr.size and arr._resident_on(dev):  # in HBM: only the results come back
+            if arr.size and (arr._resident_on(dev) or (dev is not None and arr.size <= SMALL)):
+                # in HBM (or small enough to upload): only the results come back
                 dk = context.device_key(dev)
                 if not out_origin and dtype == 'float':
                     _, f32, st = resident.decrypt_decode(dk, arr._dw(dev), arr.exponents)
