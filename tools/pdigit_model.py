@@ -291,3 +291,134 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# ---------------------------------------------------------------------------
+# Montgomery digits mod n^2 (n = p q, public): the same product with the
+# modulus n, W = 27-bit limbs and K = 80 (R = 2^2160 > 2^100 n at 2048 bits;
+# 28-bit limbs would overflow the 64-bit lazy columns at K > 41), plus the
+# conversions a kernel needs from and to plain residues mod n^2:
+#   in:  X = x + ceil(R/n) n^2  (= x mod n^2, and REDC(X) = t lands in [n, 2n+))
+#        REDC(X): X + m n = R t  ->  (t - n, R - m) are the digits of x R^-2
+#        (R (t - n) + n (R - m) = X - R n ... = x + ceil(R/n) n^2 - R n + ...;
+#        exactly: R(t-n) + n(R-m) = R t - n m = X == x (mod n^2)), then one
+#        digit product by the digits of R^2 mod n^2 (a constant row) -> x
+#   out: y0 = REDC(a) (quotient m_a, delta = [REDC(a) >= n]),
+#        y1 = (REDC(REDC(c) - m_a + R n) + delta) mod n,   y = y0 + n y1
+class NDigits(MontDigits):
+    def __init__(self, n, W_=27, K=None):
+        self.W = W_
+        self.B = 1 << W_
+        self.MASK = self.B - 1
+        self.P = n
+        self.k = K or -(-(n.bit_length() + 13) // W_)
+        self.R = 1 << (W_ * self.k)
+        self.n0inv = (-pow(n, -1, self.B)) % self.B
+        self.E = (1 - self.R) % n
+        self.Kn2 = -(-self.R // n) * n * n
+        # digits of R^2 mod n^2 (the input conversion's constant row)
+        X4 = pow(self.R, 4, n * n)
+        e = X4 * pow(self.R, -1, n) % n
+        self.w = (e, ((X4 - self.R * e) // n) % n)
+
+    def limbs(self, x):
+        out = [(x >> (self.W * i)) & self.MASK for i in range(self.k - 1)]
+        out.append(x >> (self.W * (self.k - 1)))
+        assert out[-1] < (1 << 32), "top limb overflows 32 bits"
+        return out
+
+    def redc(self, T, nlimbs, ctr):
+        """operand-scanning REDC of an nlimbs-limb value (lazy columns):
+        returns (t, m) with value + m n = R t"""
+        n, W_ = self.P, self.W
+        cols = [(T >> (W_ * i)) & self.MASK for i in range(nlimbs)]
+        cols[-1] = T >> (W_ * (nlimbs - 1))
+        cols += [0] * max(0, 2 * self.k - nlimbs)
+        m = 0
+        nl = [(n >> (W_ * j)) & self.MASK for j in range(self.k)]
+        carry = 0
+        for i in range(self.k):
+            x = cols[i] + carry
+            mi = (x * self.n0inv) & self.MASK
+            m |= mi << (W_ * i)
+            x += mi * nl[0]
+            assert x & self.MASK == 0
+            carry = x >> W_
+            for j in range(1, self.k):
+                cols[i + j] += mi * nl[j]
+                ctr.max_col = max(ctr.max_col, cols[i + j])
+            ctr.mads += self.k
+        rest = sum(cols[i] << (W_ * (i - self.k)) for i in range(self.k, len(cols))) + carry
+        assert (T + m * n) == rest * self.R
+        return rest, m
+
+    def mul(self, x, y, ctr):
+        """MontDigits.mul with this W (limbs_loose for the state)"""
+        k, n, W_ = self.k, self.P, self.W
+        (a, c), (e, f) = x, y
+        al, cl, el, fl = self.limbs(a), self.limbs(c), self.limbs(e), self.limbs(f)
+        nl = [(n >> (W_ * j)) & self.MASK for j in range(k)]
+        El = [(self.E >> (W_ * j)) & self.MASK for j in range(k)]
+        T1, T2 = [0] * k, [0] * k
+        for i in range(k):
+            x1 = T1[0] + el[i] * al[0]
+            m1 = (x1 * self.n0inv) & self.MASK
+            x1 += m1 * nl[0]
+            x2 = T2[0] + el[i] * cl[0] + fl[i] * al[0]
+            m2 = (x2 * self.n0inv) & self.MASK
+            x2 += m2 * nl[0]
+            assert x1 & self.MASK == 0 and x2 & self.MASK == 0
+            for j in range(1, k):
+                T1[j - 1] = T1[j] + el[i] * al[j] + m1 * nl[j]
+                T2[j - 1] = T2[j] + el[i] * cl[j] + fl[i] * al[j] + m2 * nl[j]
+            ctr.mads += 5 * k
+            T1[k - 1] = 0
+            T2[k - 1] = (self.MASK - m1) + El[i]
+            T1[0] += x1 >> W_
+            T2[0] += x2 >> W_
+            ctr.max_col = max(ctr.max_col, max(T1), max(T2))
+        return (sum(t << (W_ * i) for i, t in enumerate(T1)), sum(t << (W_ * i) for i, t in enumerate(T2)))
+
+    def to_digits(self, x, ctr):
+        t, m = self.redc(x + self.Kn2, 2 * self.k + 1, ctr)
+        assert self.P <= t < 2 * self.P + 2, "REDC(x + Kn2) left [n, 2n]"
+        return self.mul((t - self.P, self.R - m), self.w, ctr)
+
+    def from_digits(self, a, c, ctr):
+        n = self.P
+        ta, ma = self.redc(a, self.k, ctr)
+        assert ta <= n
+        delta = 1 if ta >= n else 0
+        y0 = ta - delta * n
+        u, _ = self.redc(c, self.k, ctr)
+        tw, _ = self.redc(u - ma + self.R * n, 2 * self.k, ctr)
+        y1 = (tw + delta) % n
+        assert tw + delta < 3 * n
+        return y0 + n * y1
+
+
+def ndigits_check(bits, trials, rng):
+    worst = 0
+    for t in range(trials):
+        n = random_prime_like(bits // 2, rng) * random_prime_like(bits // 2, rng)
+        D = NDigits(n)
+        n2 = n * n
+        ctr = Counter()
+        x = rng.randrange(n2) if t % 3 else rng.randrange(n)
+        st = D.to_digits(x, ctr)
+        assert D.value(*st) == x, "input conversion"
+        acc = x
+        for s in range(5):
+            if s % 2:
+                st = D.mul(st, st, ctr)  # squaring: the state as its own operand
+                acc = acc * acc % n2
+            else:
+                y = rng.randrange(n2)
+                st = D.mul(st, D.to_digits(y, ctr), ctr)
+                acc = acc * y % n2
+            assert D.value(*st) == acc
+            assert st[0] < 2 * n and st[1] < D.R + 6 * n, "state bounds"
+        assert D.from_digits(*st, ctr) == acc, "output conversion"
+        worst = max(worst, ctr.max_col)
+    return {"ndigit_K": D.k, "ndigit_W": D.W, "ndigit_max_column_log2": worst.bit_length(),
+            "ndigit_trials": trials}

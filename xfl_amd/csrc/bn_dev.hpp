@@ -55,6 +55,9 @@ namespace xhe {
 #ifndef XHE_PMD
 #define XHE_PMD 1  // 2048-bit DJN tables as Montgomery digits, encrypted by k_djn_pmd (pdigit_dev.hpp)
 #endif
+#ifndef XHE_NDIG
+#define XHE_NDIG 1  // 2048-bit n^2 exponentiations (public non-DJN r^n, scalar mul c^k) in Montgomery digits mod n^2
+#endif
 #ifndef XHE_APREF2
 #define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif

@@ -397,3 +397,500 @@ XHE_DEV void unpack_pairs_lds(uint32_t* slot) {
 }
 
 }  // namespace xhe
+
+namespace xhe {
+
+// ---------------------------------------------------------------------------
+// Montgomery digits mod n^2 over TPI lanes (PMDX; 2048-bit keys: K = 80
+// limbs of W = 27 bits, R = 2^2160, TPI = 4 lanes of L = 20 limbs). The same
+// representation and product as PMD with the modulus n in place of P
+// (x R^2 = R a + n c mod n^2), spread over a lane group like Mont<K, 27, TPI>:
+// lane g holds limbs [gL, (g+1)L) of a, c and of the two lazy accumulators.
+// 27-bit limbs because the columns collect 3 products of up to 2^56 per step
+// over K = 80 steps (tools/pdigit_model.py NDigits: columns below 2^62).
+// The operand (e_i, f_i) of step i is read by all lanes of the group from
+// one LDS pair (a broadcast read; `OpLds`) or from a uniform global row
+// (`OpRow`, the conversion constants); the quotient digits m1, m2 are formed
+// on lane 0 and broadcast by DPP, and each step hands the low limb of every
+// lane down to the lane before (from_next) while the lane keeps its carry -
+// the multi-lane Montgomery step of bn_dev.hpp with two accumulators.
+struct OpLds {  // pair i of a group's operand at p[i * stride]
+  const uint2* p;
+  int stride;
+  XHE_DEV uint2 load(int i) const { return p[i * stride]; }
+};
+struct OpRow {  // a uniform row of K pairs (key constants)
+  const uint2* __restrict__ p;
+  XHE_DEV uint2 load(int i) const { return p[i]; }
+};
+
+template <int K_, int TPI_>
+struct PMDX {
+  static constexpr int K = K_, TPI = TPI_, L = K_ / TPI_, W = 27;
+  static constexpr uint32_t MASK = (1u << W) - 1u;
+  using G = Grp<TPI_>;
+  using MN = Mont<K_, 27, TPI_>;  // the same limbs mod n: Montgomery products, reduce_once, I/O
+  static_assert(K_ % TPI_ == 0 && L >= 8, "lane groups of at least 8 limbs");
+  static_assert((double)K_ * (double)(5ull << 54) < 18446744073709551616.0, "accumulator bound");
+
+  MN M;  // n limbs of this lane (M.nl), n0inv
+
+  XHE_DEV void init(const uint32_t* N, uint32_t ninv) { M.init(N, ninv); }
+  XHE_DEV static bool last() { return G::g() == TPI - 1; }
+
+  // one step of the two interleaved reductions (see PMD::step); entry: x1 =
+  // T1[0] + e a[0], x2 = T2[0] + e c[0] + f a[0] (or 2e c[0]) and the
+  // broadcast digits m1, m2; the next step's x and m are formed under this
+  // step's mads. topc: MASK + E_i (used by the group's last lane).
+  template <bool SQ>
+  XHE_DEV void step(uint64_t (&T1)[L], uint64_t (&T2)[L], const uint32_t (&a)[L], const uint32_t (&c)[L],
+                    uint32_t e, uint32_t f, uint32_t en, uint32_t fn, uint32_t& m1, uint32_t& m2, uint64_t& x1,
+                    uint64_t& x2, uint32_t topc) const {
+    const uint64_t v1 = mad64(m1, M.nl[0], x1);  // lane 0: = 0 (mod 2^W)
+    const uint64_t v2 = mad64(m2, M.nl[0], x2);
+    const uint32_t e2 = e << 1;
+    uint64_t x1n = 0, x2n = 0;
+    uint32_t t1 = 0, t2 = 0;
+#pragma unroll
+    for (int j = 1; j < L; ++j) {
+      T1[j - 1] = mad64(m1, M.nl[j], mad64(e, a[j], T1[j]));
+      if constexpr (SQ) T2[j - 1] = mad64(m2, M.nl[j], mad64(e2, c[j], T2[j]));
+      else T2[j - 1] = mad64(m2, M.nl[j], mad64(f, a[j], mad64(e, c[j], T2[j])));
+      // the next step's chain, one link after each group of limbs
+      if (j == 2) {
+        T1[0] += v1 >> W;
+        T2[0] += v2 >> W;
+        asm volatile("" : "+v"(T1[0]), "+v"(T2[0]));
+      } else if (j == 5) {
+        x1n = mad64(en, a[0], T1[0]);
+        if constexpr (SQ) x2n = mad64(en << 1, c[0], T2[0]);
+        else x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
+        asm volatile("" : "+v"(x1n), "+v"(x2n));
+      } else if (j == 9) {
+        t1 = (uint32_t)x1n * M.n0inv;
+        t2 = (uint32_t)x2n * M.n0inv;
+        asm volatile("" : "+v"(t1), "+v"(t2));
+      } else if (j == 13) {
+        t1 = G::bcast0(t1 & MASK);
+        t2 = G::bcast0(t2 & MASK);
+        asm volatile("" : "+v"(t1), "+v"(t2));
+      }
+      if ((j & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    // hand the low limb of position gL down to lane g-1 (its top position);
+    // the group's last lane takes 0 (T1) and MASK - m1 + E_i (T2)
+    const uint32_t d1 = G::from_next((uint32_t)v1 & MASK);
+    const uint32_t d2 = G::from_next((uint32_t)v2 & MASK);
+    T1[L - 1] = d1;
+    T2[L - 1] = last() ? (uint64_t)(topc - m1) : (uint64_t)d2;
+    x1 = x1n;
+    x2 = x2n;
+    m1 = t1;
+    m2 = t2;
+  }
+
+  // (a, c) <- (a, c) (x) operand; SQ: the operand is (a, c) itself (parked
+  // in the group's LDS pairs by the caller), 4 K^2 instead of 5 K^2 mads
+  template <bool SQ, class OP>
+  XHE_DEV void run(uint32_t (&a)[L], uint32_t (&c)[L], const OP& op, const uint32_t* topc) const {
+    uint64_t T1[L], T2[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T1[j] = T2[j] = 0;
+    uint2 p0 = op.load(0);
+    uint64_t x1 = mad64(p0.x, a[0], 0ull);
+    uint64_t x2 = SQ ? mad64(p0.x << 1, c[0], 0ull) : mad64(p0.y, a[0], mad64(p0.x, c[0], 0ull));
+    uint32_t m1 = G::bcast0(((uint32_t)x1 * M.n0inv) & MASK), m2 = G::bcast0(((uint32_t)x2 * M.n0inv) & MASK);
+    for (int i = 0; i < K; i += 2) {
+      const uint2 tc = *reinterpret_cast<const uint2*>(topc + i);
+      const uint2 p1 = op.load(i + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      step<SQ>(T1, T2, a, c, p0.x, p0.y, p1.x, p1.y, m1, m2, x1, x2, tc.x);
+      __builtin_amdgcn_sched_barrier(0);
+      p0 = op.load(i + 2 < K ? i + 2 : i);
+      __builtin_amdgcn_sched_barrier(0);
+      step<SQ>(T1, T2, a, c, p1.x, p1.y, p0.x, p0.y, m1, m2, x1, x2, tc.y);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    normalize_top(T1, a);
+    normalize_top(T2, c);
+  }
+
+  // carry-normalise lazy columns into W-bit limbs across the group; what
+  // leaves the group's top limb stays in it (unmasked): c' may exceed R
+  XHE_DEV static void normalize_top(const uint64_t (&T)[L], uint32_t (&b)[L]) {
+    uint64_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t x = T[j] + cy;
+      b[j] = (uint32_t)x & MASK;
+      cy = x >> W;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // one round of lane-to-lane carries (cy < 2^38), then every lane's carry
+    // out is 0 or 1 and passes a lane only when all its limbs are MASK: a
+    // carry-lookahead on the wave's lane masks as Mont::normalize, except that
+    // the group's top lane keeps its carry out in its top limb
+    const bool top = last();
+    uint64_t cin = G::from_prev64(cy);
+    uint64_t out = top ? cy : 0ull;
+    uint32_t all = 1u;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t x = (uint64_t)b[j] + cin;
+      b[j] = (uint32_t)x & MASK;
+      cin = x >> W;
+      all &= (b[j] == MASK) ? 1u : 0u;
+    }
+    // generate: cin (0 or 1) leaves the lane; propagate: all limbs MASK
+    constexpr uint64_t tops = TPI == 16 ? 0x8000800080008000ull : TPI == 4 ? 0x8888888888888888ull
+                                                                            : 0xAAAAAAAAAAAAAAAAull;
+    const uint64_t gm = __builtin_amdgcn_ballot_w64(cin != 0);
+    const uint64_t pm = __builtin_amdgcn_ballot_w64(all != 0);
+    const uint64_t gi = gm & ~tops, ti = (gm | pm) & ~tops;
+    const uint64_t cm = (gi + ti) ^ gi ^ ti;  // carries into each lane (none across groups)
+    uint32_t ci = (uint32_t)(cm >> (threadIdx.x & 63)) & 1u;
+    // the top lane's own carry out: generated there, or propagated through it
+    if (top) out += cin + ((all && ci) ? 1u : 0u);
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint32_t x = b[j] + ci;
+      b[j] = x & MASK;
+      ci = x >> W;
+    }
+    if (top) b[L - 1] += (uint32_t)out << W;
+  }
+
+  // group-uniform DPP broadcast of lane k's value (k a constant after unrolling)
+  template <int k>
+  XHE_DEV static uint32_t from_lane(uint32_t v) {
+    if constexpr (TPI == 4) return G::template dpp<k | (k << 2) | (k << 4) | (k << 6)>(v);
+    else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);  // row_newbcast
+  }
+  XHE_DEV static uint32_t from_lane_i(uint32_t v, int k) {
+    static_assert(TPI == 4, "");
+    return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
+  }
+
+  // REDC with the quotient digits kept: T (lazy K-limb columns per lane) +
+  // m n = R t. HI: a 2K-limb input whose limb K + gL + j is xh[j] of lane g,
+  // entering at the group's last lane at step gL + j (else a K-limb input).
+  // On return T holds t (lazy columns) and lane g holds digits gL..gL+L-1 of
+  // m in mq.
+  // b (masked limbs, < 2^(WK)) <- b - n if b >= n; returns whether it
+  // subtracted (group-uniform). Mont::reduce_once with the flag kept.
+  XHE_DEV bool csub(uint32_t (&b)[L]) const {
+    uint32_t d[L];
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int64_t x = (int64_t)b[j] - (int64_t)M.nl[j] - (int64_t)br;
+      br = x < 0 ? 1u : 0u;
+      d[j] = (uint32_t)(x + ((int64_t)br << W));
+    }
+    uint32_t total = br;
+#pragma unroll
+    for (int r = 1; r < TPI; ++r) {
+      uint32_t bin = G::from_prev(br);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int64_t x = (int64_t)d[j] - (int64_t)bin;
+        bin = x < 0 ? 1u : 0u;
+        d[j] = (uint32_t)(x + ((int64_t)bin << W));
+      }
+      br = bin;
+      total |= bin;
+    }
+    br = G::bcast_last(total);
+    if (!br) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) b[j] = d[j];
+    }
+    return br == 0;
+  }
+
+  template <bool HI>
+  XHE_DEV void redc_q(uint64_t (&T)[L], const uint32_t (&xh)[L], uint32_t (&mq)[L]) const {
+    const int g = G::g();
+    const bool top = last();
+#pragma unroll
+    for (int ib = 0; ib < TPI; ++ib) {
+#pragma unroll
+      for (int jj = 0; jj < L; ++jj) {
+        const uint32_t m = G::bcast0(((uint32_t)T[0] * M.n0inv) & MASK);
+        mq[jj] = g == ib ? m : mq[jj];
+        const uint64_t v = mad64(m, M.nl[0], T[0]);
+#pragma unroll
+        for (int j = 1; j < L; ++j) T[j - 1] = mad64(m, M.nl[j], T[j]);
+        T[0] += v >> W;
+        const uint32_t d = G::from_next((uint32_t)v & MASK);
+        const uint32_t h = HI ? from_lane_i(xh[jj], ib) : 0u;
+        T[L - 1] = top ? (uint64_t)h : (uint64_t)d;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+};
+
+
+// ---------------------------------------------------------------------------
+// Building blocks of the PMDX kernels. Per element group: the operand pairs of
+// its products in LDS (pair i at ops[i * ostride], ostride = groups per block),
+// a table of digit states in global memory (pair i of entry t at
+// tab[(t K + i) gs], gs = group slots of the grid, tab pre-offset by the
+// group's slot).
+
+// limbs [FIRST, FIRST + L) of a little-endian word array (W-bit limbs; zero
+// beyond nwords): immediate shifts, every word loaded once
+template <int W, int L, int FIRST>
+XHE_DEV void limbs_at(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwords) {
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int bit = W * (FIRST + j), k = bit >> 5, sh = bit & 31;
+    const uint32_t lo = k < nwords ? w[k] : 0u;
+    const uint32_t hi = (sh + W > 32 && k + 1 < nwords) ? w[k + 1] : 0u;
+    b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << W) - 1u);
+  }
+}
+// lane g's limbs [BASE + gL, BASE + (g+1) L) (lane index dispatched to
+// compile-time copies, as Mont::load_words)
+template <class D, int BASE, int GG = 0>
+XHE_DEV void pmdx_load(uint32_t (&b)[D::L], const uint32_t* __restrict__ w, int nwords, int g) {
+  if constexpr (GG == D::TPI - 1) {
+    limbs_at<D::W, D::L, BASE + GG * D::L>(b, w, nwords);
+  } else {
+    if (g == GG) limbs_at<D::W, D::L, BASE + GG * D::L>(b, w, nwords);
+    else pmdx_load<D, BASE, GG + 1>(b, w, nwords, g);
+  }
+}
+
+// the per-lane table addresses are formed at each use (laundered base):
+// hoisted out of the exponentiation loop they would hold 2 VGPRs per pair
+// and the product's accumulators would spill (as opaque() in bn_dev.hpp)
+template <class T>
+XHE_DEV T* pmdx_launder(T* p) {
+  int zero = 0;
+  asm volatile("" : "+s"(zero));
+  return p + zero;
+}
+
+template <class D>
+XHE_DEV void pmdx_park(const uint32_t (&a)[D::L], const uint32_t (&c)[D::L], uint2* ops, int ostride) {
+  const int g = D::G::g();
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) ops[(g * D::L + j) * ostride] = make_uint2(a[j], c[j]);
+}
+template <class D>
+XHE_DEV void pmdx_put(const uint32_t (&a)[D::L], const uint32_t (&c)[D::L], uint2* tab, int t, int gs) {
+  const int g = D::G::g();
+  uint2* p = pmdx_launder(tab) + ((size_t)t * D::K + g * D::L) * gs;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) p[(size_t)j * gs] = make_uint2(a[j], c[j]);
+}
+template <class D>
+XHE_DEV void pmdx_get(uint32_t (&a)[D::L], uint32_t (&c)[D::L], const uint2* tab, int t, int gs) {
+  const int g = D::G::g();
+  const uint2* p = pmdx_launder(tab) + ((size_t)t * D::K + g * D::L) * gs;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) {
+    const uint2 v = p[(size_t)j * gs];
+    a[j] = v.x;
+    c[j] = v.y;
+  }
+}
+template <class D>
+XHE_DEV void pmdx_tab_to_ops(const uint2* tab, int t, int gs, uint2* ops, int ostride) {
+  const int g = D::G::g();
+  const uint2* p = pmdx_launder(tab) + ((size_t)t * D::K + g * D::L) * gs;
+  uint2 v[D::L];
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) v[j] = p[(size_t)j * gs];
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) ops[(g * D::L + j) * ostride] = v[j];
+}
+template <class D>
+XHE_DEV void pmdx_row_to_tab(const uint2* __restrict__ row, uint2* tab, int t, int gs) {
+  const int g = D::G::g();
+  uint2* p = pmdx_launder(tab) + ((size_t)t * D::K + g * D::L) * gs;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) p[(size_t)j * gs] = row[g * D::L + j];
+}
+
+// plain x (2K limbs lo | hi, W-bit, < n^2) -> its digits (a, c):
+//   X = x + ceil(R/n) n^2 (kn2, 2K limbs), REDC(X): X + m n = R t with t in
+//   [n, 2n]; (t - n, R - m) are the digits of x R^-2 (R (t - n) + n (R - m) =
+//   X - R n + n R ... = R t - n m = X = x mod n^2); one product by the digits
+//   of R^2 mod n^2 (dw) gives x's. (tools/pdigit_model.py NDigits.to_digits)
+template <class D>
+XHE_DEV void pmdx_to_digits(const D& X, const uint32_t (&lo)[D::L], const uint32_t (&hi)[D::L],
+                            const uint32_t* __restrict__ kn2, const uint32_t* __restrict__ rmn,
+                            const uint2* __restrict__ dw, const uint32_t* topc, uint32_t (&a)[D::L],
+                            uint32_t (&c)[D::L]) {
+  constexpr int L = D::L, K = D::K;
+  const int g = D::G::g();
+  uint64_t T[L];
+  uint32_t xh[L], mq[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    T[j] = (uint64_t)lo[j] + kn2[g * L + j];
+    xh[j] = hi[j] + kn2[K + g * L + j];
+    mq[j] = 0;
+  }
+  X.template redc_q<true>(T, xh, mq);
+  D::normalize_top(T, a);  // t
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[j] = (uint64_t)a[j] + rmn[g * L + j];
+  D::normalize_top(T, a);  // t - n + R
+  if (D::last()) a[L - 1] &= D::MASK;
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[j] = (uint64_t)(D::MASK - mq[j]) + ((g == 0 && j == 0) ? 1u : 0u);
+  D::normalize_top(T, c);  // R - m
+  X.template run<false>(a, c, OpRow{dw}, topc);
+}
+
+// digits (a, c) -> plain y = y0 + n y1 (y0, y1 in [0, n)):
+//   y0 = REDC(a) - delta n (quotient m_a), u = REDC(c),
+//   y1 = (REDC((u - m_a) + R n) + delta) mod n   (NDigits.from_digits)
+template <class D>
+XHE_DEV void pmdx_from_digits(const D& X, const uint32_t (&a)[D::L], const uint32_t (&c)[D::L],
+                              uint32_t (&y0)[D::L], uint32_t (&y1)[D::L]) {
+  constexpr int L = D::L;
+  const int g = D::G::g();
+  uint64_t T[L];
+  uint32_t mqa[L], xh[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    T[j] = a[j];
+    mqa[j] = 0;
+    xh[j] = 0;
+  }
+  X.template redc_q<false>(T, xh, mqa);
+  D::normalize_top(T, y0);
+  const bool delta = X.csub(y0);
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[j] = c[j];
+  X.template redc_q<false>(T, xh, y1);  // quotient not needed (y1 as scratch)
+  D::normalize_top(T, y1);              // u < n + 2
+  // s = u + (R - m_a); b = [s >= R] (u >= m_a); w = (s mod R) + R (n - 1 + b)
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[j] = (uint64_t)y1[j] + (D::MASK - mqa[j]) + ((g == 0 && j == 0) ? 1u : 0u);
+  D::normalize_top(T, y1);
+  const uint32_t b = D::G::bcast_last(D::last() ? (y1[L - 1] >> D::W) : 0u);
+  if (D::last()) y1[L - 1] &= D::MASK;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    xh[j] = X.M.nl[j];
+    T[j] = y1[j];
+  }
+  if (g == 0) xh[0] = xh[0] - 1u + b;
+  X.template redc_q<true>(T, xh, mqa);
+  D::normalize_top(T, y1);  // < 2n + 1
+  if (delta && g == 0) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = y1[j] + (j == 0 ? 1u : 0u);
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = y1[j];
+  }
+  D::normalize_top(T, y1);
+  X.M.reduce_once(y1);
+  X.M.reduce_once(y1);
+}
+
+// (a, c) <- (a, c)^E for an exponent shared by the wave (5-bit sliding
+// window, odd powers in tab entries 0..15; pmd_pow_uniform's schedule)
+template <class D>
+XHE_DEV void pmdx_pow_uniform(const D& X, uint32_t (&a)[D::L], uint32_t (&c)[D::L], const uint32_t* ex, int ebits,
+                              uint2* tab, int gs, uint2* ops, int ostride, const uint32_t* topc) {
+  auto bit = [&](int i) { return (ex[i >> 5] >> (i & 31)) & 1u; };
+  const OpLds op{ops, ostride};
+  auto square = [&]() XHE_INL {
+    pmdx_park<D>(a, c, ops, ostride);
+    wave_sync_mem_();
+    X.template run<true>(a, c, op, topc);
+    wave_sync_mem_();
+  };
+  pmdx_put<D>(a, c, tab, 0, gs);
+  square();  // x^2
+  pmdx_park<D>(a, c, ops, ostride);
+  wave_sync_mem_();
+  pmdx_get<D>(a, c, tab, 0, gs);
+#pragma unroll 1
+  for (int t = 1; t < 16; ++t) {
+    X.template run<false>(a, c, op, topc);  // x^(2t+1) = x^(2t-1) x^2
+    pmdx_put<D>(a, c, tab, t, gs);
+  }
+  wave_sync_mem_();
+  int i = ebits - 1;
+  while (i >= 0 && !bit(i)) --i;
+  int pend_sq = 0, pend_mul = -1;
+  {
+    int j = i - 4 < 0 ? 0 : i - 4;
+    while (!bit(j)) ++j;
+    uint32_t val = 0;
+    for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+    pmdx_get<D>(a, c, tab, (int)(val >> 1), gs);
+    i = j - 1;
+  }
+#pragma unroll 1
+  while (true) {
+    if (pend_sq > 0) {
+      square();
+      --pend_sq;
+    } else if (pend_mul >= 0) {
+      pmdx_tab_to_ops<D>(tab, pend_mul, gs, ops, ostride);
+      wave_sync_mem_();
+      X.template run<false>(a, c, op, topc);
+      wave_sync_mem_();
+      pend_mul = -1;
+    } else if (i < 0) {
+      break;
+    } else if (!bit(i)) {
+      pend_sq = 1;
+      --i;
+    } else {
+      int j = i - 4 < 0 ? 0 : i - 4;
+      while (!bit(j)) ++j;
+      uint32_t val = 0;
+      for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+      pend_sq = i - j + 1;
+      pend_mul = (int)(val >> 1);
+      i = j - 1;
+    }
+  }
+}
+
+// (a, c) <- (a, c)^k, k per element: 4-bit fixed windows (a uniform
+// schedule), entries x^0 (the digits of 1, d1) .. x^15 in tab
+template <class D, class DIGIT>
+XHE_DEV void pmdx_pow_window4(const D& X, uint32_t (&a)[D::L], uint32_t (&c)[D::L], int nwin, const DIGIT& digit,
+                              const uint2* __restrict__ d1, uint2* tab, int gs, uint2* ops, int ostride,
+                              const uint32_t* topc) {
+  const OpLds op{ops, ostride};
+  pmdx_row_to_tab<D>(d1, tab, 0, gs);
+  pmdx_put<D>(a, c, tab, 1, gs);
+  pmdx_park<D>(a, c, ops, ostride);
+  wave_sync_mem_();
+#pragma unroll 1
+  for (int t = 2; t < 16; ++t) {
+    X.template run<false>(a, c, op, topc);  // x^t = x^(t-1) x
+    pmdx_put<D>(a, c, tab, t, gs);
+  }
+  wave_sync_mem_();
+  pmdx_get<D>(a, c, tab, (int)digit(nwin - 1), gs);
+#pragma unroll 1
+  for (int w = nwin - 2; w >= 0; --w) {
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+      pmdx_park<D>(a, c, ops, ostride);
+      wave_sync_mem_();
+      X.template run<true>(a, c, op, topc);
+      wave_sync_mem_();
+    }
+    pmdx_tab_to_ops<D>(tab, (int)digit(w), gs, ops, ostride);
+    wave_sync_mem_();
+    X.template run<false>(a, c, op, topc);
+    wave_sync_mem_();
+  }
+}
+
+}  // namespace xhe
