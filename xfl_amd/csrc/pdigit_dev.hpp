@@ -438,49 +438,125 @@ struct PMDX {
   XHE_DEV void init(const uint32_t* N, uint32_t ninv) { M.init(N, ninv); }
   XHE_DEV static bool last() { return G::g() == TPI - 1; }
 
+  // Blocks of 4 limbs of both accumulators in one asm statement (tied in/out
+  // accumulators: T[j-1+k] is written after its old value was consumed, so
+  // the registers stay put and no rotation copies appear; one statement per
+  // block keeps the hazard nops the compiler puts after each asm low):
+  //   T1[j-1+k] = T1[j+k] + e a[j+k] + m1 n[j+k]
+  //   T2[j-1+k] = T2[j+k] + e c[j+k] + f a[j+k] + m2 n[j+k]   (SQ: 2e c[j+k] + m2 n[j+k])
+  template <bool SQ>
+  XHE_DEV void blk4(uint64_t (&T1)[L], uint64_t (&T2)[L], const uint32_t (&a)[L], const uint32_t (&c)[L],
+                    uint32_t e, uint32_t f, uint32_t m1, uint32_t m2, int j) const {
+    if constexpr (SQ) {
+      // f carries 2e
+      asm("v_mad_u64_u32 %0, vcc, %10, %14, %1\n\t"
+          "v_mad_u64_u32 %1, vcc, %10, %15, %2\n\t"
+          "v_mad_u64_u32 %2, vcc, %10, %16, %3\n\t"
+          "v_mad_u64_u32 %3, vcc, %10, %17, %8\n\t"
+          "v_mad_u64_u32 %4, vcc, %11, %18, %5\n\t"
+          "v_mad_u64_u32 %5, vcc, %11, %19, %6\n\t"
+          "v_mad_u64_u32 %6, vcc, %11, %20, %7\n\t"
+          "v_mad_u64_u32 %7, vcc, %11, %21, %9\n\t"
+          "v_mad_u64_u32 %0, vcc, %12, %22, %0\n\t"
+          "v_mad_u64_u32 %1, vcc, %12, %23, %1\n\t"
+          "v_mad_u64_u32 %2, vcc, %12, %24, %2\n\t"
+          "v_mad_u64_u32 %3, vcc, %12, %25, %3\n\t"
+          "v_mad_u64_u32 %4, vcc, %13, %22, %4\n\t"
+          "v_mad_u64_u32 %5, vcc, %13, %23, %5\n\t"
+          "v_mad_u64_u32 %6, vcc, %13, %24, %6\n\t"
+          "v_mad_u64_u32 %7, vcc, %13, %25, %7"
+          : "+v"(T1[j - 1]), "+v"(T1[j]), "+v"(T1[j + 1]), "+v"(T1[j + 2]), "+v"(T2[j - 1]), "+v"(T2[j]),
+            "+v"(T2[j + 1]), "+v"(T2[j + 2])
+          : "v"(T1[j + 3]), "v"(T2[j + 3]), "v"(e), "v"(f), "v"(m1), "v"(m2), "v"(a[j]), "v"(a[j + 1]),
+            "v"(a[j + 2]), "v"(a[j + 3]), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]), "v"(c[j + 3]), "v"(M.nl[j]),
+            "v"(M.nl[j + 1]), "v"(M.nl[j + 2]), "v"(M.nl[j + 3])
+          : "vcc");
+    } else {
+      // T1: e a + m1 n; T2: e c + f a + m2 n (a[j..] are shared by both)
+      asm("v_mad_u64_u32 %0, vcc, %10, %14, %1\n\t"
+          "v_mad_u64_u32 %1, vcc, %10, %15, %2\n\t"
+          "v_mad_u64_u32 %2, vcc, %10, %16, %3\n\t"
+          "v_mad_u64_u32 %3, vcc, %10, %17, %8\n\t"
+          "v_mad_u64_u32 %4, vcc, %10, %18, %5\n\t"
+          "v_mad_u64_u32 %5, vcc, %10, %19, %6\n\t"
+          "v_mad_u64_u32 %6, vcc, %10, %20, %7\n\t"
+          "v_mad_u64_u32 %7, vcc, %10, %21, %9\n\t"
+          "v_mad_u64_u32 %4, vcc, %11, %14, %4\n\t"
+          "v_mad_u64_u32 %5, vcc, %11, %15, %5\n\t"
+          "v_mad_u64_u32 %6, vcc, %11, %16, %6\n\t"
+          "v_mad_u64_u32 %7, vcc, %11, %17, %7\n\t"
+          "v_mad_u64_u32 %0, vcc, %12, %22, %0\n\t"
+          "v_mad_u64_u32 %1, vcc, %12, %23, %1\n\t"
+          "v_mad_u64_u32 %2, vcc, %12, %24, %2\n\t"
+          "v_mad_u64_u32 %3, vcc, %12, %25, %3\n\t"
+          "v_mad_u64_u32 %4, vcc, %13, %22, %4\n\t"
+          "v_mad_u64_u32 %5, vcc, %13, %23, %5\n\t"
+          "v_mad_u64_u32 %6, vcc, %13, %24, %6\n\t"
+          "v_mad_u64_u32 %7, vcc, %13, %25, %7"
+          : "+v"(T1[j - 1]), "+v"(T1[j]), "+v"(T1[j + 1]), "+v"(T1[j + 2]), "+v"(T2[j - 1]), "+v"(T2[j]),
+            "+v"(T2[j + 1]), "+v"(T2[j + 2])
+          : "v"(T1[j + 3]), "v"(T2[j + 3]), "v"(e), "v"(f), "v"(m1), "v"(m2), "v"(a[j]), "v"(a[j + 1]),
+            "v"(a[j + 2]), "v"(a[j + 3]), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]), "v"(c[j + 3]), "v"(M.nl[j]),
+            "v"(M.nl[j + 1]), "v"(M.nl[j + 2]), "v"(M.nl[j + 3])
+          : "vcc");
+    }
+  }
+
   // one step of the two interleaved reductions (see PMD::step); entry: x1 =
   // T1[0] + e a[0], x2 = T2[0] + e c[0] + f a[0] (or 2e c[0]) and the
   // broadcast digits m1, m2; the next step's x and m are formed under this
-  // step's mads. topc: MASK + E_i (used by the group's last lane).
+  // step's mads, one link after each block. topc: MASK + E_i (used by the
+  // group's last lane).
   template <bool SQ>
   XHE_DEV void step(uint64_t (&T1)[L], uint64_t (&T2)[L], const uint32_t (&a)[L], const uint32_t (&c)[L],
                     uint32_t e, uint32_t f, uint32_t en, uint32_t fn, uint32_t& m1, uint32_t& m2, uint64_t& x1,
                     uint64_t& x2, uint32_t topc) const {
+    static_assert((L - 1) % 4 == 3, "positions 1..L-1: 4-limb blocks and a 3-limb tail");
     const uint64_t v1 = mad64(m1, M.nl[0], x1);  // lane 0: = 0 (mod 2^W)
     const uint64_t v2 = mad64(m2, M.nl[0], x2);
-    const uint32_t e2 = e << 1;
+    // the limbs handed down to lane g-1 (DPP sources well before the DPP)
+    const uint32_t h1 = (uint32_t)v1 & MASK, h2 = (uint32_t)v2 & MASK;
+    const uint32_t f2 = SQ ? (e << 1) : f;
     uint64_t x1n = 0, x2n = 0;
-    uint32_t t1 = 0, t2 = 0;
-#pragma unroll
-    for (int j = 1; j < L; ++j) {
-      T1[j - 1] = mad64(m1, M.nl[j], mad64(e, a[j], T1[j]));
-      if constexpr (SQ) T2[j - 1] = mad64(m2, M.nl[j], mad64(e2, c[j], T2[j]));
-      else T2[j - 1] = mad64(m2, M.nl[j], mad64(f, a[j], mad64(e, c[j], T2[j])));
-      // the next step's chain, one link after each group of limbs
-      if (j == 2) {
+    uint32_t t1 = 0, t2 = 0, d1 = 0, d2 = 0;
+    int stage = 0;
+    auto advance = [&]() XHE_INL {
+      if (stage == 0) {
         T1[0] += v1 >> W;
         T2[0] += v2 >> W;
         asm volatile("" : "+v"(T1[0]), "+v"(T2[0]));
-      } else if (j == 5) {
+      } else if (stage == 1) {
         x1n = mad64(en, a[0], T1[0]);
         if constexpr (SQ) x2n = mad64(en << 1, c[0], T2[0]);
         else x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
         asm volatile("" : "+v"(x1n), "+v"(x2n));
-      } else if (j == 9) {
+      } else if (stage == 2) {
         t1 = (uint32_t)x1n * M.n0inv;
         t2 = (uint32_t)x2n * M.n0inv;
-        asm volatile("" : "+v"(t1), "+v"(t2));
-      } else if (j == 13) {
+        d1 = G::from_next(h1);
+        d2 = G::from_next(h2);
+        asm volatile("" : "+v"(t1), "+v"(t2), "+v"(d1), "+v"(d2));
+      } else if (stage == 3) {
         t1 = G::bcast0(t1 & MASK);
         t2 = G::bcast0(t2 & MASK);
         asm volatile("" : "+v"(t1), "+v"(t2));
       }
-      if ((j & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      ++stage;
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int j = 1;
+#pragma unroll
+    for (; j + 4 <= L; j += 4) {
+      blk4<SQ>(T1, T2, a, c, e, f2, m1, m2, j);
+      advance();
     }
-    // hand the low limb of position gL down to lane g-1 (its top position);
-    // the group's last lane takes 0 (T1) and MASK - m1 + E_i (T2)
-    const uint32_t d1 = G::from_next((uint32_t)v1 & MASK);
-    const uint32_t d2 = G::from_next((uint32_t)v2 & MASK);
+#pragma unroll
+    for (; j < L; ++j) {  // the tail
+      T1[j - 1] = mad64(m1, M.nl[j], mad64(e, a[j], T1[j]));
+      if constexpr (SQ) T2[j - 1] = mad64(m2, M.nl[j], mad64(f2, c[j], T2[j]));
+      else T2[j - 1] = mad64(m2, M.nl[j], mad64(f, a[j], mad64(e, c[j], T2[j])));
+    }
+    while (stage < 4) advance();
     T1[L - 1] = d1;
     T2[L - 1] = last() ? (uint64_t)(topc - m1) : (uint64_t)d2;
     x1 = x1n;
