@@ -55,6 +55,9 @@ namespace xhe {
 #ifndef XHE_PMD
 #define XHE_PMD 1  // 2048-bit DJN tables as Montgomery digits, encrypted by k_djn_pmd (pdigit_dev.hpp)
 #endif
+#ifndef XHE_PMDX
+#define XHE_PMDX 1  // 3072/4096-bit DJN tables as Montgomery digits, encrypted by k_djn_pmdx over 4 lanes
+#endif
 #ifndef XHE_NDIG
 #define XHE_NDIG 1  // 2048-bit n^2 exponentiations (public non-DJN r^n, scalar mul c^k) in Montgomery digits mod n^2
 #endif

@@ -511,7 +511,7 @@ struct PMDX {
   XHE_DEV void step(uint64_t (&T1)[L], uint64_t (&T2)[L], const uint32_t (&a)[L], const uint32_t (&c)[L],
                     uint32_t e, uint32_t f, uint32_t en, uint32_t fn, uint32_t& m1, uint32_t& m2, uint64_t& x1,
                     uint64_t& x2, uint32_t topc) const {
-    static_assert((L - 1) % 4 == 3, "positions 1..L-1: 4-limb blocks and a 3-limb tail");
+    static_assert(L >= 8, "positions 1..L-1: 4-limb blocks and a tail");
     const uint64_t v1 = mad64(m1, M.nl[0], x1);  // lane 0: = 0 (mod 2^W)
     const uint64_t v2 = mad64(m2, M.nl[0], x2);
     // the limbs handed down to lane g-1 (DPP sources well before the DPP)
@@ -783,6 +783,38 @@ XHE_DEV void pmdx_tab_to_ops(const uint2* tab, int t, int gs, uint2* ops, int os
 #pragma unroll
   for (int j = 0; j < D::L; ++j) ops[(g * D::L + j) * ostride] = v[j];
 }
+// digit states in HBM between kernels: pair i of element e at st[i count + e]
+template <class D>
+XHE_DEV void ndig_st_store(const uint32_t (&a)[D::L], const uint32_t (&c)[D::L], uint2* st, int64_t count, int64_t e) {
+  const int g = D::G::g();
+  uint2* p = pmdx_launder(st) + e;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) p[(size_t)(g * D::L + j) * count] = make_uint2(a[j], c[j]);
+}
+template <class D>
+XHE_DEV void ndig_st_load(uint32_t (&a)[D::L], uint32_t (&c)[D::L], const uint2* st, int64_t count, int64_t e) {
+  const int g = D::G::g();
+  const uint2* p = pmdx_launder(st) + e;
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) {
+    const uint2 v = p[(size_t)(g * D::L + j) * count];
+    a[j] = v.x;
+    c[j] = v.y;
+  }
+}
+
+// a packed digit row (e in words [0, hw), f in [hw, 2 hw), little-endian) into
+// the group's operand pairs (each lane unpacks its own limbs)
+template <class D>
+XHE_DEV void pmdx_stage_row(const uint32_t* __restrict__ row, int hw, uint2* ops, int ostride) {
+  const int g = D::G::g();
+  uint32_t le[D::L], lf[D::L];
+  pmdx_load<D, 0>(le, row, hw, g);
+  pmdx_load<D, 0>(lf, row + hw, hw, g);
+#pragma unroll
+  for (int j = 0; j < D::L; ++j) ops[(g * D::L + j) * ostride] = make_uint2(le[j], lf[j]);
+}
+
 template <class D>
 XHE_DEV void pmdx_row_to_tab(const uint2* __restrict__ row, uint2* tab, int t, int gs) {
   const int g = D::G::g();

@@ -55,6 +55,7 @@ struct Shape3072 {
   using MP = Mont<56, 28, 2>;
   using MN2 = Mont<228, 27, 4>;
   using MN2X = Mont<240, 27, 16>;
+  using PDX = PMDX<60, 4>;  // Montgomery digits mod p^2, q^2 (k_djn_pmdx)
 };
 // 4096-bit keys (the LR/LinReg/Pearson/WoE operators' OneOf(2048, 4096, 8192)):
 // 28-bit limbs would overflow the lazy 64-bit accumulator at S = 147
@@ -70,6 +71,7 @@ struct Shape4096 {
   using MP = Mont<76, 27, 4>;
   using MN2 = Mont<304, 27, 16>;
   using MN2X = Mont<304, 27, 16>;
+  using PDX = PMDX<80, 4>;
 };
 
 // 8192-bit keys: p^2 (8192 bits) in one 16-lane row of 27-bit limbs, p in 4
@@ -358,6 +360,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
     size_t topc_p = 0, topc_q = 0;
+    ModOff xd[2];
+    size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
   } o;
   int pm1_bits = 0, qm1_bits = 0, ep_bits = 0, eq_bits = 0;
   if (k->priv) {
@@ -446,6 +450,46 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       o.topc_q = topc(Q);
     }
 #endif
+#if XHE_PMDX
+    if (k->djn && (K == 3072 || K == 4096)) {
+      // Montgomery digits mod P^2 over 4 lanes (k_djn_pmdx): per prime the
+      // modulus P in K limbs of 27 bits (R = 2^(27 K)), ceil(R/P) P^2, R - P,
+      // MASK + E_i, the fold constant Q R^3 mod P and the digits of
+      // R^2 R_MP2^-1 mod P^2 (R_MP2: the MP2 shape's R, the tables' factor)
+      const int KD = K == 3072 ? 60 : 80;
+      const ModSpec sd{KD, 27};
+      const BigU Rd = pow2((size_t)27 * KD), RM = pow2((size_t)s2.W * s2.S);
+      for (int i = 0; i < 2; ++i) {
+        const BigU& X = i ? Q : P;
+        const BigU& Y = i ? P : Q;
+        const BigU X2 = i ? q2 : p2;
+        o.xd[i] = put_mod(bl, X, sd);
+        BigU cq;
+        divmod(sub(add(Rd, X), BigU(1)), X, &cq, nullptr);
+        o.xkn2[i] = bl.put_limbs(mul(cq, X2), ModSpec{2 * KD, 27});
+        o.xrmn[i] = bl.put_limbs(sub(Rd, X), sd);
+        const BigU RdX = mod(Rd, X);
+        std::vector<uint32_t> tc = submod(BigU(1), RdX, X).to_limbs(27, KD);
+        for (auto& x : tc) x += (1u << 27) - 1u;
+        o.xtopc[i] = bl.put(tc);
+        o.xfold[i] = bl.put_limbs(mulmod(mod(Y, X), mulmod(mulmod(RdX, RdX, X), RdX, X), X), sd);
+        // digits (e, f) of w = R^2 R_MP2^-1 mod X^2: R e + X f = w R^2 (mod X^2)
+        const BigU Rd2 = mulmod(mod(Rd, X2), mod(Rd, X2), X2);
+        const BigU Xw = mulmod(mulmod(Rd2, Rd2, X2), modinv(mod(RM, X2), X2), X2);
+        const BigU e = mulmod(mod(Xw, X), modinv(RdX, X), X);
+        BigU Qd;
+        divmod(add(Xw, mul(Rd, sub(X, e))), X, &Qd, nullptr);
+        const BigU f = submod(mod(Qd, X), RdX, X);
+        const std::vector<uint32_t> el = e.to_limbs(27, KD), fl = f.to_limbs(27, KD);
+        std::vector<uint32_t> v(2 * KD);
+        for (int j = 0; j < KD; ++j) {
+          v[2 * j] = el[j];
+          v[2 * j + 1] = fl[j];
+        }
+        o.xdwt[i] = bl.put(v);
+      }
+    }
+#endif
     o.p2x = bl.put_limbs(shl(P, 1), s1);
     o.p_lim = bl.put_limbs(P, s1);
     // non-DJN private obfuscation exponents ep = n mod phi(p^2) (context.py:51-52)
@@ -529,6 +573,22 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       kd.topc_q = B + o.topc_q;
     }
 #endif
+#if XHE_PMDX
+    if (k->djn && (K == 3072 || K == 4096)) {
+      kd.dp = moddev(B, o.xd[0]);
+      kd.dq = moddev(B, o.xd[1]);
+      kd.x_kn2_p = B + o.xkn2[0];
+      kd.x_kn2_q = B + o.xkn2[1];
+      kd.x_rmn_p = B + o.xrmn[0];
+      kd.x_rmn_q = B + o.xrmn[1];
+      kd.x_topc_p = B + o.xtopc[0];
+      kd.x_topc_q = B + o.xtopc[1];
+      kd.x_fold_p = B + o.xfold[0];
+      kd.x_fold_q = B + o.xfold[1];
+      kd.x_dwt_p = reinterpret_cast<const uint2*>(B + o.xdwt[0]);
+      kd.x_dwt_q = reinterpret_cast<const uint2*>(B + o.xdwt[1]);
+    }
+#endif
     if (k->djn) {
       kd.win = win & 0xff;
       win_layout(k->rand_bits, kd.win, (win & XHE_WIN_SPLIT) != 0, &kd.nwin, &kd.nhi);
@@ -562,6 +622,25 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
                              mp[i].N, mp[i].n0inv, mp[i].R1, tabs[i], trows, (int64_t)kd.tab_rs);
           HIPCHK(hipGetLastError());
         }
+        HIPCHK(hipDeviceSynchronize());
+      }
+#endif
+#if XHE_PMDX
+      if (K == 3072 || K == 4096) {
+        // rows as Montgomery digits (e, f) for k_djn_pmdx
+        kd.pmdx = 1;
+        const int64_t trows = (int64_t)(kd.nwin + kd.nhi) << kd.win;
+        with_shape(K, [&](auto sh) {
+          using Sh = decltype(sh);
+          if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+            using D = typename Sh::PDX;
+            for (int i = 0; i < 2; ++i) {
+              hipLaunchKernelGGL((k_tab_to_pmdx<D, Sh::RW>), dim3((unsigned)((trows * D::TPI + 127) / 128)),
+                                 dim3(128), 0, nullptr, kd, i, tabs[i], trows, (int64_t)kd.tab_rs);
+              HIPCHK(hipGetLastError());
+            }
+          }
+        });
         HIPCHK(hipDeviceSynchronize());
       }
 #endif
@@ -718,6 +797,8 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
   ws_alloc((void**)&ws, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s);
+  uint2* xst = nullptr;  // k_djn_pmdx workspaces (allocated on first use)
+  uint32_t *xrows = nullptr, *xwords = nullptr;
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     int blocks = (int)((n * MP2::TPI + 255) / 256);
@@ -736,6 +817,33 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
         if (G == 16) launch(k_djn_pmd<MP2, 37, Sh::RW, 16>);
         else if (G == 4) launch(k_djn_pmd<MP2, 37, Sh::RW, 4>);
         else launch(k_djn_pmd<MP2, 37, Sh::RW, 1>);
+        HIPCHK(hipGetLastError());
+        crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
+        continue;
+      }
+    }
+#endif
+#if XHE_PMDX
+    if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+      if (k->kd.pmdx) {
+        using D = typename Sh::PDX;
+        if (!xst) {
+          ws_alloc((void**)&xst, (size_t)2 * D::K * chunk * sizeof(uint2), s);
+          ws_alloc((void**)&xrows, (size_t)2 * 2 * D::MN::S4 * chunk * sizeof(uint32_t), s);
+          ws_alloc((void**)&xwords, (size_t)2 * chunk * Sh::RW * sizeof(uint32_t), s);
+        }
+        const dim3 g4((unsigned)((n * D::TPI + 127) / 128), 2);
+        {
+          ProfScope ps("k_djn_pow", s);
+          hipLaunchKernelGGL((k_djn_pmdx<D, Sh::RW>), g4, dim3(128), 0, s, k->kd, r + (size_t)off * k->rand_words,
+                             k->rand_words, n, xst);
+          HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL((k_pmdx_enc_out<D, Sh::RW>), g4, dim3(128), 0, s, k->kd, m + (size_t)off * k->nw, n, xst,
+                           xrows, xwords);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_words_to_rows<MP2>, dim3((unsigned)((n * MP2::TPI + 255) / 256), 2), dim3(256), 0, s,
+                           xwords, Sh::RW, n, ws);
         HIPCHK(hipGetLastError());
         crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
         continue;
@@ -770,6 +878,11 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
   }
   ws_free(ws, s);
+  if (xst) {
+    ws_free(xst, s);
+    ws_free(xrows, s);
+    ws_free(xwords, s);
+  }
 }
 
 // grid for per-group-workspace (grid-stride) kernels

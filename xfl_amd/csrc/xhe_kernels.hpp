@@ -83,6 +83,14 @@ struct KeyDev {
   ModDev nd;
   const uint32_t *nd_kn2, *nd_rmn, *nd_topc;
   const uint2 *nd_dw, *nd_d1;
+  // ---- Montgomery digits mod P^2 over 4 lanes (PMDX, 3072/4096-bit DJN
+  // private keys; k_djn_pmdx): P as K limbs of 27 bits, ceil(R/P) P^2, R - P,
+  // MASK + E_i, the fold constant Q R^3 mod P (Q the other prime) and the
+  // digits of R^2 R_MP2^-1 mod P^2 (the table rows' conversion constant)
+  int pmdx;
+  ModDev dp, dq;
+  const uint32_t *x_kn2_p, *x_kn2_q, *x_rmn_p, *x_rmn_q, *x_topc_p, *x_topc_q, *x_fold_p, *x_fold_q;
+  const uint2 *x_dwt_p, *x_dwt_q;
 };
 
 // ============================================================== encode
@@ -814,6 +822,185 @@ XHE_DEV void pmd_pow_uniform(const PMD<KP>& M, uint32_t (&a)[KP], uint32_t (&c)[
     if (!next_op()) break;
   }
 #undef tab
+}
+
+// ---------------------------------------------------------------------------
+// DJN encryption in Montgomery digits over 4 lanes (PMDX, 3072/4096-bit keys;
+// the one-lane k_djn_pmd's construction with the multi-lane product of
+// k_ndig_*): the tables hold each row as its digits (e, f) < P (RW/2 words
+// each, k_tab_to_pmdx); per prime and element group the first window's row is
+// the start state and every further row is unpacked into the group's LDS
+// pairs and multiplied in. k_pmdx_enc_out then leaves digits (from_digits),
+// folds in (1 + n m) in base P - (1 + n m) y = y0 + P ((y1 + y0 Q m) mod P),
+// Q the other prime, as y0 Q m = MontMul(MontMul(y0, REDC(m)), Q R^3) - and
+// writes c_P's words; k_words_to_rows puts them into the MP2 rows k_crt_enc
+// reads. Digit state between the kernels: st [prime][pair i][count].
+template <class D>
+struct PmdxKey {
+  const ModDev& md;
+  const uint32_t *kn2, *rmn, *topc, *fold;
+  const uint2* dwt;
+  XHE_DEV PmdxKey(const KeyDev& k, int prime)
+      : md(prime ? k.dq : k.dp),
+        kn2(prime ? k.x_kn2_q : k.x_kn2_p),
+        rmn(prime ? k.x_rmn_q : k.x_rmn_p),
+        topc(prime ? k.x_topc_q : k.x_topc_p),
+        fold(prime ? k.x_fold_q : k.x_fold_p),
+        dwt(prime ? k.x_dwt_q : k.x_dwt_p) {}
+};
+
+template <class D, int RW>
+__global__ void __launch_bounds__(128, 2) k_djn_pmdx(KeyDev key, const uint32_t* __restrict__ a_words, int aw,
+                                                     int64_t count, uint2* __restrict__ st) {
+  constexpr int GPB = 128 / D::TPI, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  const int prime = blockIdx.y;
+  const PmdxKey<D> pk(key, prime);
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = pk.topc[i];
+  __syncthreads();
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  D X;
+  X.init(pk.md.N, pk.md.n0inv);
+  uint32_t a[L], c[L];
+  {
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, 0, row0);
+    const uint32_t* row = tab + (size_t)(row0 + d) * key.tab_rs;
+    pmdx_load<D, 0>(a, row, RW / 2, g);
+    pmdx_load<D, 0>(c, row + RW / 2, RW / 2, g);
+  }
+  for (int w = 1; w < key.nwin; ++w) {
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    pmdx_stage_row<D>(pmdx_launder(tab) + (size_t)(row0 + d) * key.tab_rs, RW / 2, ops, GPB);
+    wave_sync_mem_();
+    X.template run<false>(a, c, OpLds{ops, GPB}, topc);
+    wave_sync_mem_();
+  }
+  ndig_st_store<D>(a, c, st + (size_t)prime * D::K * count, count, e);
+}
+
+template <class D, int RW>
+__global__ void __launch_bounds__(128, 2) k_pmdx_enc_out(KeyDev key, const uint32_t* __restrict__ m_words,
+                                                         int64_t count, const uint2* __restrict__ st,
+                                                         uint32_t* __restrict__ rows27, uint32_t* __restrict__ words) {
+  constexpr int L = D::L, S4 = D::MN::S4;
+  const int prime = blockIdx.y;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  const PmdxKey<D> pk(key, prime);
+  D X;
+  X.init(pk.md.N, pk.md.n0inv);
+  uint32_t y0[L], y1[L];
+  {
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, st + (size_t)prime * D::K * count, count, e);
+    pmdx_from_digits(X, a, c, y0, y1);
+  }
+  const int cnt = (int)count;
+  uint32_t* rows = rows27 + (size_t)prime * 2 * S4 * count + e;
+  {  // y1 <- (y1 + y0 Q m) mod P
+    uint32_t lo[L], hi[L], mq[L];
+    const uint32_t* me = m_words + (size_t)e * key.nw;
+    pmdx_load<D, 0>(lo, me, key.nw, g);
+    pmdx_load<D, D::K>(hi, me, key.nw, g);
+    uint64_t T[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      T[j] = lo[j];
+      mq[j] = 0;
+    }
+    X.template redc_q<true>(T, hi, mq);
+    D::normalize_top(T, lo);  // m R^-1 mod P (< 2P)
+    uint32_t* trow = rows + (size_t)S4 * count;
+    X.M.store_strided(lo, trow, cnt);
+    wave_sync_mem_();
+#pragma unroll
+    for (int j = 0; j < L; ++j) lo[j] = y0[j];
+    X.M.mul(lo, AStrided{trow, cnt});  // y0 m R^-2
+    X.M.mul(lo, ARow{pk.fold});        // y0 m Q (< 2P)
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = (uint64_t)y1[j] + lo[j];
+    D::normalize_top(T, y1);
+    X.M.reduce_once(y1);
+    X.M.reduce_once(y1);
+  }
+  X.M.store_strided(y0, rows, cnt);
+  wave_sync_mem_();
+  X.M.wide_mul_add_store(y1, ARow{pk.md.N}, rows, cnt, words + ((size_t)prime * count + e) * RW, RW);
+}
+
+// c_P words [prime][count][nwords] -> the MP2 rows of k_crt_enc ([prime][2 S4][count])
+template <class MP2>
+__global__ void __launch_bounds__(256, 2) k_words_to_rows(const uint32_t* __restrict__ words, int nwords,
+                                                          int64_t count, uint32_t* __restrict__ ws) {
+  const int prime = blockIdx.y;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2::TPI;
+  if (e >= count) return;
+  MP2 N;
+  uint32_t b[MP2::L];
+  N.load_words(b, words + ((size_t)prime * count + e) * nwords, nwords);
+  N.store_strided(b, ws + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
+}
+
+// Table rows X = x R_MP2 mod P^2 (packed RW words, reduced) -> the digits
+// (e, f) of x, RW/2 words each, in place: to_digits with the constant
+// digits of R^2 R_MP2^-1 (one group of TPI lanes per row)
+template <class D, int RW>
+__global__ void __launch_bounds__(128, 2) k_tab_to_pmdx(KeyDev key, int prime, uint32_t* __restrict__ tab,
+                                                        int64_t rows, int64_t rs) {
+  constexpr int GPB = 128 / D::TPI, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  const PmdxKey<D> pk(key, prime);
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = pk.topc[i];
+  __syncthreads();
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (r >= rows) return;
+  const int g = D::G::g();
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  uint32_t* row = tab + (size_t)r * rs;
+  D X;
+  X.init(pk.md.N, pk.md.n0inv);
+  uint32_t a[L], c[L];
+  {
+    uint32_t lo[L], hi[L];
+    pmdx_load<D, 0>(lo, row, RW, g);
+    pmdx_load<D, D::K>(hi, row, RW, g);
+    pmdx_to_digits(X, lo, hi, pk.kn2, pk.rmn, pk.dwt, topc, a, c);
+  }
+  // canonical digits for the packed row (a product leaves a < P(1 + 2P/R)
+  // and c < R + 4P, which would not fit RW/2 words): a - kP and (c + kR) mod
+  // P (R (a - P) + P (c + R) = R a + P c), the latter as MontMul(REDC(c + kR),
+  // R^2) = (c + kR) mod P
+  {
+    const bool k = X.csub(a);
+    uint64_t T[L];
+    uint32_t zero[L], mq[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      T[j] = c[j];
+      zero[j] = 0;
+      mq[j] = 0;
+    }
+    if (k && D::last()) T[L - 1] += (uint64_t)1 << D::W;
+    X.template redc_q<false>(T, zero, mq);
+    D::normalize_top(T, c);
+    X.M.mul(c, ARow{pk.md.R2});
+    X.M.reduce_once(c);
+  }
+  pmdx_park<D>(a, c, ops, GPB);
+  wave_sync_mem_();
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(ops);
+  pack_words_<D::W, D::TPI>(lds, 2 * GPB, D::K, row, RW / 2);
+  pack_words_<D::W, D::TPI>(lds + 1, 2 * GPB, D::K, row + RW / 2, RW / 2);
 }
 
 // k_dec_pow (one lane per residue) in Montgomery digits, as three kernels so
@@ -1607,25 +1794,6 @@ struct NdigWs {
   static constexpr size_t tab_bytes_per_slot() { return (size_t)16 * D::K * 8; }
 };
 
-template <class D>
-XHE_DEV void ndig_st_store(const uint32_t (&a)[D::L], const uint32_t (&c)[D::L], uint2* st, int64_t count, int64_t e) {
-  const int g = D::G::g();
-  uint2* p = pmdx_launder(st) + e;
-#pragma unroll
-  for (int j = 0; j < D::L; ++j) p[(size_t)(g * D::L + j) * count] = make_uint2(a[j], c[j]);
-}
-template <class D>
-XHE_DEV void ndig_st_load(uint32_t (&a)[D::L], uint32_t (&c)[D::L], const uint2* st, int64_t count, int64_t e) {
-  const int g = D::G::g();
-  const uint2* p = pmdx_launder(st) + e;
-#pragma unroll
-  for (int j = 0; j < D::L; ++j) {
-    const uint2 v = p[(size_t)(g * D::L + j) * count];
-    a[j] = v.x;
-    c[j] = v.y;
-  }
-}
-
 // x (WIDE: n2w ciphertext words, else nwords words of a value < n) -> digits
 template <class D, bool WIDE>
 __global__ void __launch_bounds__(128, 2) k_ndig_in(KeyDev key, const uint32_t* __restrict__ x, int nwords,
@@ -2153,25 +2321,41 @@ __global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __
   int neg = cmpw(m, key.minneg) >= 0;
   int32_t st = 0;
   if (!neg && cmpw(m, key.maxpos) > 0) st = 1;
-  // magnitude: top 128 bits window of |v|
-  // find bit length
-  int bl = 0;
-  // |v| = neg ? n - m : m ; compute words on the fly from the top
-  // (borrow needs low words, so compute full magnitude into a small cache)
-  // Word k of |v| without materialising it (nw reaches 256 at 8192 bits):
-  // for v = m - n the borrow into word k is [m mod 2^(32k) > n mod 2^(32k)],
-  // decided by the highest differing word below k (almost always k - 1).
-  auto magw = [&](int k) -> uint32_t {
-    if (!neg) return m[k];
-    uint32_t br = 0;
-    for (int j = k - 1; j >= 0; --j)
-      if (m[j] != key.n_words[j]) { br = m[j] > key.n_words[j]; break; }
-    return key.n_words[k] - m[k] - br;
-  };
-  for (int k = nw - 1; k >= 0; --k) {
-    const uint32_t w = magw(k);
-    if (w) { bl = 32 * k + 32 - __clz(w); break; }
+  // |v| (neg: n - m) in ONE forward pass over the words, with its borrow
+  // chain: the four words ending at the highest nonzero one (w4[3] = word hk)
+  // and the OR of every word below them (the rounding's sticky part). (Word
+  // by word from the top, each word's borrow needed a scan of the words below
+  // it: O(nw^2) loads per element, 0.2 ms for the LR demo's 15 gradients.)
+  uint32_t w4[4] = {0u, 0u, 0u, 0u};
+  uint32_t low_or = 0u, br = 0u;
+  int hk = -1;
+  for (int k = 0; k < nw; ++k) {
+    uint32_t w;
+    if (neg) {
+      const uint64_t d = (uint64_t)key.n_words[k] - (uint64_t)m[k] - br;
+      w = (uint32_t)d;
+      br = (uint32_t)(d >> 63);
+    } else {
+      w = m[k];
+    }
+    if (w) {
+      const int g = k - hk;  // >= 1: words hk+1 .. k-1 are zero
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < g) low_or |= w4[t];  // leaves the window
+      uint32_t nw4[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) nw4[t] = t == 3 ? w : (t + g <= 3 ? w4[t + g] : 0u);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w4[t] = nw4[t];
+      hk = k;
+    }
   }
+  const int bl = hk < 0 ? 0 : 32 * hk + 32 - __clz(w4[3]);
+  auto magw = [&](int k) -> uint32_t {  // word k of |v| for k >= hk - 3
+    const int t = 3 - (hk - k);
+    return (k > hk || t < 0) ? 0u : w4[t];
+  };
   double res;
   if (st != 0) { res = 0.0; }
   else if (bl == 0) {
@@ -2186,18 +2370,20 @@ __global__ void k_decode(const uint32_t* __restrict__ m_words, const int32_t* __
       shift = 0;
     } else {
       int s = bl - 53;
-      // extract 53 bits starting at bit s, plus round/sticky
+      // extract 53 bits starting at bit s, plus round/sticky (all inside the
+      // window: s - 1 >= 32 hk - 53)
       auto bitsat = [&](int pos) -> uint64_t {  // 64 bits starting at pos
         int k = pos >> 5, o = pos & 31;
-        uint64_t w0 = k < nw ? magw(k) : 0, w1 = k + 1 < nw ? magw(k + 1) : 0, w2 = k + 2 < nw ? magw(k + 2) : 0;
+        uint64_t w0 = magw(k), w1 = magw(k + 1), w2 = magw(k + 2);
         uint64_t lo = (w0 | (w1 << 32)) >> o;
         if (o) lo |= w2 << (64 - o);
         return lo;
       };
       mant = bitsat(s) & ((1ull << 53) - 1);
       uint64_t rbit = (bitsat(s - 1) & 1ull);
-      bool sticky = false;
-      for (int k = 0; k < ((s - 1) >> 5); ++k) sticky |= magw(k) != 0;
+      bool sticky = low_or != 0;
+      for (int k = hk - 3; k < ((s - 1) >> 5); ++k)
+        if (k >= 0) sticky |= magw(k) != 0;
       int sb = (s - 1) & 31;
       if (sb) sticky |= (magw((s - 1) >> 5) & ((1u << sb) - 1u)) != 0;
       shift = s;
