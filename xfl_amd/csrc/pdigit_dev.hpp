@@ -640,11 +640,13 @@ struct PMDX {
   template <int k>
   XHE_DEV static uint32_t from_lane(uint32_t v) {
     if constexpr (TPI == 4) return G::template dpp<k | (k << 2) | (k << 4) | (k << 6)>(v);
+    else if constexpr (TPI == 2) return G::template dpp<k | (k << 2) | ((2 + k) << 4) | ((2 + k) << 6)>(v);
     else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);  // row_newbcast
   }
   XHE_DEV static uint32_t from_lane_i(uint32_t v, int k) {
-    static_assert(TPI == 4, "");
-    return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
+    static_assert(TPI == 4 || TPI == 2, "");
+    if constexpr (TPI == 2) return k == 0 ? from_lane<0>(v) : from_lane<1>(v);
+    else return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
   }
 
   // REDC with the quotient digits kept: T (lazy K-limb columns per lane) +

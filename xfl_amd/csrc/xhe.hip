@@ -55,7 +55,8 @@ struct Shape3072 {
   using MP = Mont<56, 28, 2>;
   using MN2 = Mont<228, 27, 4>;
   using MN2X = Mont<240, 27, 16>;
-  using PDX = PMDX<60, 4>;  // Montgomery digits mod p^2, q^2 (k_djn_pmdx)
+  using PDX = PMDX<60, 2>;   // Montgomery digits mod p^2, q^2: k_djn_pmdx's products (2 lanes of 30 limbs)
+  using PDXO = PMDX<60, 4>;  // its conversions (k_pmdx_enc_out, k_tab_to_pmdx; 2 lanes would spill there)
 };
 // 4096-bit keys (the LR/LinReg/Pearson/WoE operators' OneOf(2048, 4096, 8192)):
 // 28-bit limbs would overflow the lazy 64-bit accumulator at S = 147
@@ -72,6 +73,7 @@ struct Shape4096 {
   using MN2 = Mont<304, 27, 16>;
   using MN2X = Mont<304, 27, 16>;
   using PDX = PMDX<80, 4>;
+  using PDXO = PMDX<80, 4>;
 };
 
 // 8192-bit keys: p^2 (8192 bits) in one 16-lane row of 27-bit limbs, p in 4
@@ -633,7 +635,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
         with_shape(K, [&](auto sh) {
           using Sh = decltype(sh);
           if constexpr (Sh::K == 3072 || Sh::K == 4096) {
-            using D = typename Sh::PDX;
+            using D = typename Sh::PDXO;
             for (int i = 0; i < 2; ++i) {
               hipLaunchKernelGGL((k_tab_to_pmdx<D, Sh::RW>), dim3((unsigned)((trows * D::TPI + 127) / 128)),
                                  dim3(128), 0, nullptr, kd, i, tabs[i], trows, (int64_t)kd.tab_rs);
@@ -829,7 +831,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
         using D = typename Sh::PDX;
         if (!xst) {
           ws_alloc((void**)&xst, (size_t)2 * D::K * chunk * sizeof(uint2), s);
-          ws_alloc((void**)&xrows, (size_t)2 * 2 * D::MN::S4 * chunk * sizeof(uint32_t), s);
+          ws_alloc((void**)&xrows, (size_t)2 * 2 * Sh::PDXO::MN::S4 * chunk * sizeof(uint32_t), s);
           ws_alloc((void**)&xwords, (size_t)2 * chunk * Sh::RW * sizeof(uint32_t), s);
         }
         const dim3 g4((unsigned)((n * D::TPI + 127) / 128), 2);
@@ -839,8 +841,9 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
                              k->rand_words, n, xst);
           HIPCHK(hipGetLastError());
         }
-        hipLaunchKernelGGL((k_pmdx_enc_out<D, Sh::RW>), g4, dim3(128), 0, s, k->kd, m + (size_t)off * k->nw, n, xst,
-                           xrows, xwords);
+        using DO = typename Sh::PDXO;  // the same state layout ([pair][count]) whatever the lanes per element
+        hipLaunchKernelGGL((k_pmdx_enc_out<DO, Sh::RW>), dim3((unsigned)((n * DO::TPI + 127) / 128), 2), dim3(128), 0,
+                           s, k->kd, m + (size_t)off * k->nw, n, xst, xrows, xwords);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_words_to_rows<MP2>, dim3((unsigned)((n * MP2::TPI + 255) / 256), 2), dim3(256), 0, s,
                            xwords, Sh::RW, n, ws);
