@@ -1,0 +1,422 @@
+// One-wave decrypt exponentiation for small batches (2048-bit keys).
+//
+// k_dec_pow spreads a residue's Montgomery product over at most one 16-lane
+// DPP row: its K-step operand-scanning loop is a chain of dependent
+// quotient digits (mad -> mul -> row broadcast -> hand-down), ~130 cycles a
+// step, and a 15-element decrypt (the LR demo's batch, SURVEY.md cfg 1) waits
+// ~1,210 such products. Here a whole 64-lane wave works on one residue
+// mod P^2 and the product has no serial digit chain:
+//
+//   T = a b          column sums, lane l owns columns l and l + K
+//   m = (T mod R) N' mod R          (N' = -N^-1 mod R, low columns only)
+//   x = (T + m N) / R               exact: U = T + m N = 0 (mod R)
+//
+// (Montgomery's REDC as three column products, R = 2^(28 K); the same limbs
+// and R as the one-lane MP2 shape Mont<74, 28, 1>, so the rows it writes are
+// k_dec_pow's.) Column c of a b is sum_t a_t b_(c-t): with the multiplicand
+// stored zero-padded in LDS as Z = (0^K, b, 0^K), lane l accumulates
+// a_t Z[K + l - t] (column l) and a_t Z[2K + l - t] (column l + K) for t =
+// 0..K-1 - wave-uniform a_t (an LDS broadcast), immediate LDS offsets, no
+// selects, K terms per pair. Pairs l >= 64 (K = 74: ten of them) are cut
+// into chunks of CH terms spread over the threads and added in with LDS
+// atomics.
+//
+// Column sums are lazy 64-bit (74 products below 2^56 + carries < 2^64) and
+// normalised by passes that move each column's upper bits one and two limbs
+// up (no carry chain): limbs end at most MASK + 2, which keeps the next
+// product's columns in range. Dropping what crosses limb K - 1 keeps a value
+// mod R (m and T mod R need no more); the exact U / R needs only whether the
+// low part's remainder is 0 or R after two passes - one ballot. Ranges: inputs
+// < 2N (R > 2^24 N), so T / R < N / 2^22, m < R (1 + 2^-26) and U / R < 2N.
+#pragma once
+#include "bn_dev.hpp"
+
+namespace xhe {
+
+#ifndef XHE_WAVE_FUSE
+#define XHE_WAVE_FUSE 0  // 1: T mod R and m reduced on the fly inside the products (no limb passes)
+#endif
+#ifndef XHE_WAVE_PROF
+#define XHE_WAVE_PROF 0  // dev builds: cycles per phase of block (0, 0), printed at the end
+#endif
+#if XHE_WAVE_PROF
+__device__ unsigned long long g_wave_prof[8];
+__device__ unsigned long long g_wave_t;
+#define XHE_WAVE_T(ph)                                                         \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {              \
+      const unsigned long long now_ = clock64();                               \
+      if ((ph) >= 0) g_wave_prof[(ph)] += now_ - g_wave_t;                     \
+      g_wave_t = now_;                                                         \
+    }                                                                          \
+  } while (0)
+#else
+#define XHE_WAVE_T(ph) \
+  do {                 \
+  } while (0)
+#endif
+
+// NWV waves per residue: each wave takes a quarter (NWV = 4) of the terms of
+// every column pair and adds its partial sums into the LDS columns with
+// 64-bit LDS atomics, so a product's latency is NWV times shorter than one
+// wave's and the waves' LDS waits overlap on the CU's four SIMDs.
+template <int K, int NWV>
+struct WaveMont {
+  static constexpr int W = 28;
+  static constexpr uint32_t MASK = (1u << W) - 1u;
+  static constexpr int NT = 64 * NWV;  // threads per residue
+  static constexpr int NX = K - 64;    // column pairs beyond one wave's lanes
+  static_assert(NX >= 0 && NX <= 16, "64 to 80 limbs");
+  // terms per chunk of an extra pair: the smallest with NX * ceil(K / CH) <= NT
+  static constexpr int chunk_terms() {
+    int ch = 1;
+    while (NX * ((K + ch - 1) / ch) > NT) ++ch;
+    return ch;
+  }
+  static constexpr int CH = NX ? chunk_terms() : 1;
+  static constexpr int NCH = (K + CH - 1) / CH;              // chunks per extra pair
+  static constexpr int span(int tm) { return ((tm + NWV - 1) / NWV + 3) & ~3; }  // terms per wave
+  static constexpr int mx(int a, int b) { return a > b ? a : b; }
+  // operand rows (zero beyond K): the waves' spans and the chunks may run past K
+  static constexpr int KP = (mx(mx(K, NWV * span(K)), NCH * CH) + 3) & ~3;
+  static constexpr int G = 3;  // zero guards below column 0
+
+  struct Lds {  // operand rows first: 16-byte aligned for the broadcast quad reads
+    uint32_t x[KP], r3[KP], one[KP], tl[KP], mq[KP];
+    uint32_t tab[16][KP];  // odd powers x^(2t+1)
+    uint32_t zb[3 * K];    // (0^K, b, 0^K): the multiplicand of the next product
+    uint32_t zn[3 * K];    // N, Z-padded (m N)
+    uint32_t znp[3 * K];   // N' = -N^-1 mod R, Z-padded (m = T N')
+    uint64_t col[2][G + 2 * K];  // column sums (T, then U = T + m N); two buffers, one zeroed ahead
+    uint64_t mcol[G + KP + 4];   // columns of m (norm_range reads up to KP)
+  };
+
+  static XHE_DEV int tid() { return (int)threadIdx.x; }
+  static XHE_DEV void sync() { __syncthreads(); }
+
+  // acc[k] += a_k b_k, k = 0..3: four independent accumulators in one asm
+  // statement (no dependent mads back to back, no hazard nops between them)
+  static XHE_DEV void mad4(uint64_t (&acc)[4], uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0,
+                           uint32_t b1, uint32_t b2, uint32_t b3) {
+    asm("v_mad_u64_u32 %0, vcc, %4, %8, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %5, %9, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %6, %10, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %7, %11, %3"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+        : "vcc");
+  }
+
+  // limb j of the three-way split of columns (exact: sum lim_j 2^(W j) = sum col_j 2^(W j))
+  static XHE_DEV uint32_t split3(const uint64_t* cg, int j) {
+    const uint64_t c0 = cg[j], c1 = cg[j - 1], c2 = cg[j - 2];
+    return ((uint32_t)c0 & MASK) + ((uint32_t)(c1 >> W) & MASK) + (uint32_t)(c2 >> (2 * W));
+  }
+  // limb j after a second pass (<= MASK + 2); cg = col + G, j >= 0
+  static XHE_DEV uint32_t norm(const uint64_t* cg, int j) {
+    return (split3(cg, j) & MASK) + (split3(cg, j - 1) >> W);
+  }
+  // limbs t0 .. t0 + NN - 1 of (columns mod R): norm() over a range, each
+  // column read once; zero from limb K on
+  template <int NN>
+  static XHE_DEV void norm_range(const uint64_t* cg, int t0, uint32_t (&out)[NN]) {
+    uint64_t c[NN + 3];
+#pragma unroll
+    for (int i = 0; i < NN + 3; ++i) c[i] = cg[t0 - 3 + i];
+    uint32_t lim[NN + 1];  // split3 of columns t0 - 1 ..
+#pragma unroll
+    for (int i = 0; i < NN + 1; ++i)
+      lim[i] = ((uint32_t)c[i + 2] & MASK) + ((uint32_t)(c[i + 1] >> W) & MASK) + (uint32_t)(c[i] >> (2 * W));
+#pragma unroll
+    for (int i = 0; i < NN; ++i) out[i] = t0 + i < K ? (lim[i + 1] & MASK) + (lim[i] >> W) : 0u;
+  }
+
+  // col += a x b (b in z, Z-padded; col zeroed, or holding T): HI adds the
+  // upper columns, TM bounds the terms of the main pairs (64 when only the
+  // low columns are wanted: lane l <= 63 has no low term beyond t = l). NA:
+  // a is given as lazy columns (a + G), reduced mod R on the fly (the limbs
+  // of T mod R and of m are never stored). Wave w takes terms [w S, (w+1) S)
+  // of pairs 0..63 (a is zero beyond K, and a zero a_t meets whatever z holds
+  // below its row); the extra pairs are cut into chunks of CH terms over all
+  // threads.
+  template <bool HI, int TM, bool NA>
+  static XHE_DEV void prod(const void* asrc, const uint32_t* z, uint64_t* col) {
+    constexpr int S = span(TM);
+    const int l = tid() & 63, t0 = __builtin_amdgcn_readfirstlane(tid() >> 6) * S;
+    uint32_t av[S];
+    if constexpr (NA) {
+      norm_range<S>(static_cast<const uint64_t*>(asrc), t0, av);
+    } else {
+      const uint32_t* ap = static_cast<const uint32_t*>(asrc) + t0;
+#pragma unroll
+      for (int r = 0; r < S; r += 4) {
+        const uint4 a4 = *reinterpret_cast<const uint4*>(ap + r);
+        av[r] = a4.x;
+        av[r + 1] = a4.y;
+        av[r + 2] = a4.z;
+        av[r + 3] = a4.w;
+      }
+    }
+    uint64_t lo[4] = {0ull, 0ull, 0ull, 0ull}, hi[4] = {0ull, 0ull, 0ull, 0ull};
+    const uint32_t* zl = z + l - t0;
+#pragma unroll
+    for (int r = 0; r < S; r += 4) {
+      uint32_t zlo[4], zhi[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        zlo[q] = zl[K - r - q];
+        if constexpr (HI) zhi[q] = zl[2 * K - r - q];
+      }
+      mad4(lo, av[r], av[r + 1], av[r + 2], av[r + 3], zlo[0], zlo[1], zlo[2], zlo[3]);
+      if constexpr (HI) mad4(hi, av[r], av[r + 1], av[r + 2], av[r + 3], zhi[0], zhi[1], zhi[2], zhi[3]);
+    }
+    // chunk h of extra pair 64 + xi: terms h CH .. h CH + CH - 1
+    uint64_t elo = 0, ehi = 0;
+    const int xi = tid() / NCH, h = tid() - xi * NCH;
+    const bool xl = NX > 0 && xi < NX;
+    const int c = 64 + xi, c0 = h * CH;
+    if (xl) {
+      uint32_t ax[CH];
+      if constexpr (NA) {
+        norm_range<CH>(static_cast<const uint64_t*>(asrc), c0, ax);
+      } else {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) ax[q] = static_cast<const uint32_t*>(asrc)[c0 + q];
+      }
+      const uint32_t* zp = z + (K + c - c0 - (CH - 1));
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        elo = mad64(ax[q], zp[CH - 1 - q], elo);
+        if constexpr (HI) ehi = mad64(ax[q], zp[K + CH - 1 - q], ehi);
+      }
+    }
+    atomicAdd((unsigned long long*)&col[G + l], (unsigned long long)((lo[0] + lo[1]) + (lo[2] + lo[3])));
+    if constexpr (HI)
+      atomicAdd((unsigned long long*)&col[G + K + l], (unsigned long long)((hi[0] + hi[1]) + (hi[2] + hi[3])));
+    if (xl) {
+      atomicAdd((unsigned long long*)&col[G + c], (unsigned long long)elo);
+      if constexpr (HI) atomicAdd((unsigned long long*)&col[G + K + c], (unsigned long long)ehi);
+    }
+    sync();
+  }
+
+  // dst = U / R from the columns of U = T + m N (= 0 mod R); zeroes the
+  // other column buffer and mcol for the next product. The low part reduced
+  // twice, L = sum v_j 2^(W j) (v_j <= MASK + 2), is 0 or R; if R then
+  // v_(K-1) >= MASK - 1 (the limbs below sum to < 2^(W (K-1)) (1 + 3/MASK)),
+  // else every v_j is 0: the carry out of the low part is v_(K-1) != 0, which
+  // every thread reads for itself (no ballot).
+  static XHE_DEV void tail(Lds& s, int cur, uint32_t* dst, bool zbw) {
+    const uint64_t* cg = s.col[cur] + G;
+    const uint32_t k = norm(cg, K - 1) != 0u ? 1u : 0u;
+    const uint32_t e0 = (split3(cg, K - 1) >> W) + k;  // into limb 0 of U / R
+    for (int i = tid(); i < K; i += NT) {
+      const uint32_t hi = split3(cg, K + i) + (i == 0 ? e0 : 0u);
+      const uint32_t hp = i == 0 ? 0u : split3(cg, K + i - 1) + (i == 1 ? e0 : 0u);
+      const uint32_t v = (hi & MASK) + (hp >> W);
+      dst[i] = v;
+      if (zbw) s.zb[K + i] = v;
+    }
+    for (int j = tid(); j < 2 * K; j += NT) s.col[cur ^ 1][G + j] = 0ull;
+    for (int j = tid(); j < K; j += NT) s.mcol[G + j] = 0ull;
+    sync();
+  }
+
+  // out = columns [0, K) mod R as limbs <= MASK + 2
+  static XHE_DEV void norm_low(const uint64_t* col, uint32_t* out) {
+    for (int j = tid(); j < K; j += NT) out[j] = norm(col + G, j);
+    sync();
+  }
+
+  // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N)
+  static XHE_DEV void reduce(Lds& s, int cur, uint32_t* dst, bool zbw) {
+#if XHE_WAVE_FUSE
+    prod<false, 64, true>(s.col[cur] + G, s.znp, s.mcol);  // m = (T mod R) N' mod R
+    XHE_WAVE_T(1);
+    prod<true, K, true>(s.mcol + G, s.zn, s.col[cur]);     // U = T + m N
+    XHE_WAVE_T(2);
+#else
+    norm_low(s.col[cur], s.tl);
+    prod<false, 64, false>(s.tl, s.znp, s.mcol);  // m = (T mod R) N' mod R
+    XHE_WAVE_T(1);
+    norm_low(s.mcol, s.mq);
+    prod<true, K, false>(s.mq, s.zn, s.col[cur]);  // U = T + m N
+    XHE_WAVE_T(2);
+#endif
+    tail(s, cur, dst, zbw);
+    XHE_WAVE_T(3);
+  }
+
+  // dst = a b R^-1 mod N (< 2N), b in s.zb; zbw: the result also becomes the
+  // next multiplicand. cur flips (the product's columns go to the zeroed buffer).
+  static XHE_DEV void mul(Lds& s, int& cur, const uint32_t* a, uint32_t* dst, bool zbw) {
+    cur ^= 1;
+    XHE_WAVE_T(-1);
+    prod<true, K, false>(a, s.zb, s.col[cur]);
+    XHE_WAVE_T(0);
+    reduce(s, cur, dst, zbw);
+  }
+
+  static XHE_DEV void copy_in(uint32_t* dst, const uint32_t* src, int n) {
+    for (int j = tid(); j < n; j += NT) dst[j] = src[j];
+  }
+};
+
+#ifndef XHE_DEC_NWV
+#define XHE_DEC_NWV 4  // waves per residue of k_dec_wave
+#endif
+
+// k_dec_wave: X_P = (c^(P-1) mod P^2) - 1 for one residue per block of NWV
+// waves (grid (count, 2): blockIdx.y is the prime), rows as k_dec_pow<MP2, 0>
+// writes them ([prime][xs4][count], limbs beyond K zero). Same window
+// schedule as pow_uniform_exp (5-bit sliding window over P - 1, 16 odd powers
+// in LDS), one product site.
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_t* __restrict__ c_words,
+                                                       int64_t count, int xs4, uint32_t* __restrict__ xrows) {
+  using WM = WaveMont<K, NWV>;
+  constexpr uint32_t MASK = WM::MASK;
+#if XHE_WAVE_PROF
+  if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+    for (int q = 0; q < 7; ++q) g_wave_prof[q] = 0;
+    g_wave_prof[7] = clock64();
+  }
+#endif
+  constexpr int NT = WM::NT;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int l = WM::tid();
+  const int prime = blockIdx.y;
+  const int64_t e = blockIdx.x;
+  const ModDev& md = prime ? key.q2 : key.p2;
+  const uint32_t* np = prime ? key.q2_nprime : key.p2_nprime;
+  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
+  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
+  {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+    for (int j = l; j < (int)(sizeof(s) / 4); j += NT) w[j] = 0u;
+  }
+  WM::sync();
+  for (int j = l; j < K; j += NT) {
+    s.zn[K + j] = md.N[j];
+    s.znp[K + j] = np[j];
+    s.r3[j] = md.R3[j];
+  }
+  if (l == 0) s.one[0] = 1u;
+  int cur = 0;
+  {  // c (n2w words, < 2^(28 * 2K)) as 2K limbs in the columns
+    const uint32_t* cw = c_words + (size_t)e * key.n2w;
+    const int n2w = key.n2w;
+    for (int j = l; j < 2 * K; j += NT) {
+      const int bit = 28 * j, k = bit >> 5, sh = bit & 31;
+      const uint32_t lo = k < n2w ? cw[k] : 0u, hw = k + 1 < n2w ? cw[k + 1] : 0u;
+      s.col[cur][WM::G + j] = (uint32_t)((((uint64_t)hw << 32) | lo) >> sh) & MASK;
+    }
+  }
+  WM::sync();
+  WM::reduce(s, cur, s.x, true);  // c R^-1 mod P^2
+
+  // exponent bits k in (32 (wi - 1), 32 wi + 31] from two words (wi = i >> 5)
+  auto bits64 = [&](int i, int& base) {
+    const int wi = i >> 5;
+    base = (wi - 1) * 32;
+    return ((uint64_t)ex[wi] << 32) | (wi > 0 ? ex[wi - 1] : 0u);
+  };
+  int i = ebits - 1;
+  while (i >= 0 && !((ex[i >> 5] >> (i & 31)) & 1u)) --i;
+  int step = 0, pend_sq = 0, pend_mul = -1;
+  bool fin = false;
+#pragma unroll 1
+  while (true) {
+    const uint32_t* a;
+    uint32_t* dst = s.x;
+    bool zbw = true;
+    if (step == 0) {  // c R^-1 R^3 R^-1 = c R
+      a = s.r3;
+      step = 1;
+    } else if (step == 1) {  // tab[0] = x; x = zb = x^2
+      WM::copy_in(s.tab[0], s.x, K);
+      WM::sync();
+      a = s.x;
+      step = 2;
+    } else if (step < 17) {  // tab[t] = tab[t-1] x^2 (x^2 stays in zb)
+      a = s.tab[step - 2];
+      dst = s.tab[step - 1];
+      zbw = false;
+      ++step;
+    } else if (pend_sq > 0) {
+      a = s.x;
+      --pend_sq;
+    } else if (pend_mul >= 0) {
+      a = s.tab[pend_mul];
+      pend_mul = -1;
+    } else if (i >= 0) {
+      int base;
+      const uint64_t v = bits64(i, base);
+      auto bit = [&](int k) { return (uint32_t)(v >> (k - base)) & 1u; };
+      if (step == 17 || bit(i)) {  // a window [i..j] ending in a set bit
+        int j = i - 4 < 0 ? 0 : i - 4;
+        while (!bit(j)) ++j;
+        uint32_t val = 0;
+        for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
+        if (step == 17) {  // the first window's odd power is the start value
+          WM::copy_in(s.x, s.tab[val >> 1], K);
+          WM::copy_in(s.zb + K, s.tab[val >> 1], K);
+          WM::sync();
+          step = 18;
+        } else {
+          pend_sq = i - j + 1;
+          pend_mul = (int)(val >> 1);
+        }
+        i = j - 1;
+      } else {
+        pend_sq = 1;
+        --i;
+      }
+      continue;
+    } else if (!fin) {  // x R^-1: out of Montgomery form
+      a = s.one;
+      fin = true;
+    } else {
+      break;
+    }
+    WM::mul(s, cur, a, dst, zbw);
+  }
+
+  // x < 2N in limbs <= MASK + 2: normalise, subtract N once if x >= N, then
+  // X = x - 1 mod 2^(28 K) (x = 1 mod P), written by thread 0
+  if (l == 0) {
+    uint32_t v[K];
+    uint32_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t t = s.x[j] + cy;
+      v[j] = t & MASK;
+      cy = t >> 28;
+    }
+    int64_t br = 0;
+    uint32_t d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t t = (int64_t)v[j] - (int64_t)md.N[j] - br;
+      br = t < 0 ? 1 : 0;
+      d[j] = (uint32_t)(t + (br << 28));
+    }
+    const bool ge = br == 0;
+    br = 1;  // minus one
+    uint32_t* out = xrows + (size_t)prime * xs4 * count + e;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t t = (int64_t)(ge ? d[j] : v[j]) - br;
+      br = t < 0 ? 1 : 0;
+      out[(size_t)j * count] = (uint32_t)(t + (br << 28));
+    }
+    for (int j = K; j < xs4; ++j) out[(size_t)j * count] = 0u;
+#if XHE_WAVE_PROF
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+      printf("wave prof (cycles, all products): prod1 %llu prod2 %llu prod3 %llu tail %llu total %llu\n",
+             g_wave_prof[0], g_wave_prof[1] - 0, g_wave_prof[2], g_wave_prof[3], clock64() - g_wave_prof[7]);
+#endif
+  }
+}
+
+}  // namespace xhe

@@ -19,6 +19,7 @@
 #include "abi_common.hpp"
 #include "hostbn.hpp"
 #include "xhe_kernels.hpp"
+#include "dec_wave.hpp"
 
 using namespace xhe;
 
@@ -362,6 +363,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
     size_t topc_p = 0, topc_q = 0;
+    size_t nprime_p2 = 0, nprime_q2 = 0;
     ModOff xd[2];
     size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
   } o;
@@ -377,6 +379,11 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     o.p2X = put_mod(bl, p2, k->mp2X);
     o.q2X = put_mod(bl, q2, k->mp2X);
     o.q2 = put_mod(bl, q2, s2);
+    if (K == 2048) {  // -P^-2 mod R for k_dec_wave's parallel REDC
+      const BigU R = pow2((size_t)s2.W * s2.S);
+      o.nprime_p2 = bl.put_limbs(sub(R, modinv(p2, R)), s2);
+      o.nprime_q2 = bl.put_limbs(sub(R, modinv(q2, R)), s2);
+    }
     BigU R2p = pow2((size_t)s2.W * s2.S);
     BigU Rp2 = mod(R2p, p2), Rq2 = mod(R2p, q2);
     // n R^2 mod P^2
@@ -569,6 +576,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.eq_words = B + o.eq;
     kd.ep_bits = ep_bits;
     kd.eq_bits = eq_bits;
+    if (K == 2048) {
+      kd.p2_nprime = B + o.nprime_p2;
+      kd.q2_nprime = B + o.nprime_q2;
+    }
 #if XHE_PMD && XHE_LDS_ROWS
     if (K == 2048) {
       kd.topc_p = B + o.topc_p;
@@ -1307,13 +1318,16 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
 // 11.3/11.8/11.9 ms for 4 lanes; 4 lanes 20-21 ms at 16 k vs 36 ms for 1
 // lane, 40 ms at 32 k vs 37 ms). $XHE_DEC_TPI (1, 4 or 16) pins one shape.
 constexpr int64_t kDecRowMax = 5120;
+// One 64-lane wave per residue (k_dec_wave, 2048-bit keys) up to kDecWaveMax
+// elements; $XHE_DEC_TPI=64 pins it.
+constexpr int64_t kDecWaveMax = 512;
 constexpr int64_t kDecQuadMax = 28672;
 
 int dec_tpi_override() {
   static const int v = [] {
     const char* e = std::getenv("XHE_DEC_TPI");
     int t = e ? std::atoi(e) : 0;
-    return (t == 1 || t == 4 || t == 16) ? t : 0;
+    return (t == 1 || t == 4 || t == 16 || t == 64) ? t : 0;
   }();
   return v;
 }
@@ -1372,7 +1386,9 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
   // Multi-lane key sizes take the 4-lane shape for every larger batch: at 3072
   // bits the 2-lane batch shape (55 limbs per lane) decrypted 25.5 k/s where
   // 4096 bits in 4 lanes reach 133 k/s (profiles/r1/keysizes/).
-  const int tpi = pin ? pin
+  constexpr bool wave_ok = Sh::K == 2048;
+  const int tpi = pin ? (pin == 64 && !wave_ok ? 16 : pin)
+                      : (wave_ok && count <= kDecWaveMax)          ? 64
                       : count <= kDecRowMax                        ? 16
                       : (count <= kDecQuadMax || MP2::TPI > 1) ? 4
                                                                    : 1;
@@ -1383,7 +1399,14 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     const uint32_t* cto = ct + (size_t)off * k->n2w;
-    if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
+    if (tpi == 64) {
+      if constexpr (wave_ok) {
+        static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave shares the MP2 limbs");
+        ProfScope ps("k_dec_wave", s);
+        hipLaunchKernelGGL((k_dec_wave<74, XHE_DEC_NWV>), dim3((unsigned)n, 2), dim3(64 * XHE_DEC_NWV), 0, s, k->kd, cto, n, (int)MP2::S4, xrows);
+        HIPCHK(hipGetLastError());
+      }
+    } else if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
     else if (tpi == 4) dec_pow_launch<typename Sh::MP2L, 1, MP2>(k, cto, n, chunk, xrows, s);
 #if XHE_PMD && XHE_LDS_ROWS
     else if constexpr (Sh::K == 2048) dec_pmd_launch<MP2>(k, cto, n, chunk, xrows, s);

@@ -91,6 +91,9 @@ struct KeyDev {
   ModDev dp, dq;
   const uint32_t *x_kn2_p, *x_kn2_q, *x_rmn_p, *x_rmn_q, *x_topc_p, *x_topc_q, *x_fold_p, *x_fold_q;
   const uint2 *x_dwt_p, *x_dwt_q;
+  // ---- one-wave decrypt exponentiation (k_dec_wave, 2048-bit keys): the
+  // full Montgomery inverse -P^-2 mod R of the MP2 shape (R = 2^(28*74))
+  const uint32_t *p2_nprime, *q2_nprime;
 };
 
 // ============================================================== encode
