@@ -102,11 +102,12 @@ def test_host_encrypt_chunking_is_invisible():
 
 
 @pytest.mark.parametrize("fx", FIXTURES)
-@pytest.mark.parametrize("count", [1, 300, 5000, 20000, 30000])
+@pytest.mark.parametrize("count", [1, 300, 600, 5000, 20000, 30000])
 def test_decrypt_shapes_bit_exact(fx, count):
-    """The decrypt exponentiation runs in three lane shapes chosen by batch
-    size (16 lanes per residue up to 5,120 elements, 4 up to 28,672, then 1):
-    the golden ciphertexts tiled to each regime decrypt to the golden m."""
+    """The decrypt exponentiation runs in four lane shapes chosen by batch
+    size (2048-bit keys: a 4-wave block per residue up to 512 elements, then
+    16 lanes per residue up to 5,120, 4 up to 28,672, then 1): the golden
+    ciphertexts tiled to each regime decrypt to the golden m."""
     from xfl_amd._native import ints_to_words, words_to_ints
     g = load_fixture(fx)
     dk = _dkey(g)
@@ -119,3 +120,25 @@ def test_decrypt_shapes_bit_exact(fx, count):
     cw = ints_to_words((raws * reps)[:count], dk.n2w)
     out = words_to_ints(dk.decrypt_words(cw))
     assert out == (ms * reps)[:count]
+
+
+@pytest.mark.parametrize("count", [7, 700])
+def test_decrypt_arbitrary_residues(count):
+    """Any c < n^2 coprime to n (as every ciphertext is), not only
+    well-formed ciphertexts, decrypts as the reference's arithmetic does
+    (paillier.py:341-368, restated by oracle.decrypt_raw): edge residues (1,
+    n^2 - 1, next to p^2 and q^2) and random ones, in the small-batch
+    (whole-wave) and the 16-lane shapes."""
+    import random
+
+    from xfl_amd._native import ints_to_words, words_to_ints
+    g = load_fixture("paillier_2048_djn.json")
+    dk = _dkey(g)
+    ok = _okey(g)
+    p, q, n = hx(g["key"]["p"]), hx(g["key"]["q"]), hx(g["key"]["n"])
+    n2 = n * n
+    rnd = random.Random(count)
+    edge = [1, n2 - 1, p * p - 1, p * p + 1, q * q - 2, q * q + 3, n + 1, p * q * q + 5]
+    cs = (edge + [rnd.randrange(1, n2) for _ in range(count)])[:count]
+    out = words_to_ints(dk.decrypt_words(ints_to_words(cs, dk.n2w)))
+    assert out == [O.decrypt_raw(ok, c) for c in cs]

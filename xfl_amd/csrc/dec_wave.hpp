@@ -33,9 +33,6 @@
 
 namespace xhe {
 
-#ifndef XHE_WAVE_FUSE
-#define XHE_WAVE_FUSE 0  // 1: T mod R and m reduced on the fly inside the products (no limb passes)
-#endif
 #ifndef XHE_WAVE_PROF
 #define XHE_WAVE_PROF 0  // dev builds: cycles per phase of block (0, 0), printed at the end
 #endif
@@ -56,39 +53,42 @@ __device__ unsigned long long g_wave_t;
   } while (0)
 #endif
 
-// NWV waves per residue: each wave takes a quarter (NWV = 4) of the terms of
-// every column pair and adds its partial sums into the LDS columns with
-// 64-bit LDS atomics, so a product's latency is NWV times shorter than one
-// wave's and the waves' LDS waits overlap on the CU's four SIMDs.
+// NWV waves per residue (NT threads). A product's columns are summed by
+// thread (q, s): columns 4q..4q+3 over terms t in [s TS, (s+1) TS), NQF
+// column quads of the full product (NQL of the low-only quotient product) by
+// NS term slices, added into the LDS columns with 64-bit LDS atomics. Thread
+// (q, s) reads its TS/4 quads of a and TS/4 + 1 aligned quads of the
+// zero-padded multiplicand (term quads u and u + 1 share one): 9 LDS reads
+// for 64 mads, all in flight at once. The slices run past K (a is zero there)
+// and the quads past the triangle of nonzero terms (z is zero there): 2.2x
+// the mads of the exact column sums, cheap next to the LDS round trips that
+// set a product's latency.
 template <int K, int NWV>
 struct WaveMont {
   static constexpr int W = 28;
   static constexpr uint32_t MASK = (1u << W) - 1u;
   static constexpr int NT = 64 * NWV;  // threads per residue
-  static constexpr int NX = K - 64;    // column pairs beyond one wave's lanes
-  static_assert(NX >= 0 && NX <= 16, "64 to 80 limbs");
-  // terms per chunk of an extra pair: the smallest with NX * ceil(K / CH) <= NT
-  static constexpr int chunk_terms() {
-    int ch = 1;
-    while (NX * ((K + ch - 1) / ch) > NT) ++ch;
-    return ch;
-  }
-  static constexpr int CH = NX ? chunk_terms() : 1;
-  static constexpr int NCH = (K + CH - 1) / CH;              // chunks per extra pair
-  static constexpr int span(int tm) { return ((tm + NWV - 1) / NWV + 3) & ~3; }  // terms per wave
-  static constexpr int mx(int a, int b) { return a > b ? a : b; }
-  // operand rows (zero beyond K): the waves' spans and the chunks may run past K
-  static constexpr int KP = (mx(mx(K, NWV * span(K)), NCH * CH) + 3) & ~3;
-  static constexpr int G = 3;  // zero guards below column 0
+  static constexpr int TS = 16;
+  static constexpr int NS = (K + TS - 1) / TS;
+  static constexpr int NQF = (2 * K - 1 + 3) / 4, NQL = (K + 3) / 4;
+  static_assert(NQF * NS <= NT, "one (quad, slice) per thread");
+  static_assert(K < NT, "one limb per thread in the passes");
+  static constexpr int KP = (NS * TS + 3) & ~3;  // operand rows, zero from K to the last slice's end
+  static constexpr int G = 3;                    // zero guards below column 0
+  // multiplicand rows Z: b at [ZO, ZO + K), zeros around it (reads reach
+  // ZO - NS TS - 4 .. ZO + 4 NQF)
+  static constexpr int ZO = (NS * TS + 4 + 3) & ~3;
+  static constexpr int ZS = (ZO + 4 * NQF + 4 + 3) & ~3;
 
   struct Lds {  // operand rows first: 16-byte aligned for the broadcast quad reads
     uint32_t x[KP], r3[KP], one[KP], tl[KP], mq[KP];
     uint32_t tab[16][KP];  // odd powers x^(2t+1)
-    uint32_t zb[3 * K];    // (0^K, b, 0^K): the multiplicand of the next product
-    uint32_t zn[3 * K];    // N, Z-padded (m N)
-    uint32_t znp[3 * K];   // N' = -N^-1 mod R, Z-padded (m = T N')
+    uint32_t zb[ZS];   // (0^ZO, b, 0...): the multiplicand of the next product
+    uint32_t zn[ZS];   // N, Z-padded (m N)
+    uint32_t znp[ZS];  // N' = -N^-1 mod R, Z-padded (m = T N')
     uint64_t col[2][G + 2 * K];  // column sums (T, then U = T + m N); two buffers, one zeroed ahead
-    uint64_t mcol[G + KP + 4];   // columns of m (norm_range reads up to KP)
+    uint64_t mcol[G + 4 * NQL];  // columns of m
+    uint32_t exw[64];            // the exponent P - 1 (<= 2048 bits)
   };
 
   static XHE_DEV int tid() { return (int)threadIdx.x; }
@@ -116,92 +116,42 @@ struct WaveMont {
   static XHE_DEV uint32_t norm(const uint64_t* cg, int j) {
     return (split3(cg, j) & MASK) + (split3(cg, j - 1) >> W);
   }
-  // limbs t0 .. t0 + NN - 1 of (columns mod R): norm() over a range, each
-  // column read once; zero from limb K on
-  template <int NN>
-  static XHE_DEV void norm_range(const uint64_t* cg, int t0, uint32_t (&out)[NN]) {
-    uint64_t c[NN + 3];
+  // col += a x b over quad columns (see TS above): thread (q, s) reads its
+  // slice of a as TS/4 quads and the multiplicand as TS/4 + 1 aligned quads
+  // (consecutive term quads share one), 4 TS mads into four accumulators
+  // (one per column), then one LDS atomic per column. LO: columns < K + 2
+  // only (the quotient product; its columns from K on are never read).
+  template <bool LO>
+  static XHE_DEV void prodq(const uint32_t* a, const uint32_t* z, uint64_t* col) {
+    constexpr int NQ = LO ? NQL : NQF;
+    const int q = tid() % NQ, sl = tid() / NQ;
+    if (sl < NS) {
+      const int t0 = sl * TS;
+      uint4 av[TS / 4], zq[TS / 4 + 1];
 #pragma unroll
-    for (int i = 0; i < NN + 3; ++i) c[i] = cg[t0 - 3 + i];
-    uint32_t lim[NN + 1];  // split3 of columns t0 - 1 ..
+      for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
+      // quad u of terms needs Z[B_u - 4 .. B_u + 3], B_u = ZO + 4q - t0 - 4u:
+      // zq[u + 1] = Z[B_u - 4 ..], zq[u] = Z[B_u ..]
+      const uint32_t* zb0 = z + (ZO + 4 * q - t0);
 #pragma unroll
-    for (int i = 0; i < NN + 1; ++i)
-      lim[i] = ((uint32_t)c[i + 2] & MASK) + ((uint32_t)(c[i + 1] >> W) & MASK) + (uint32_t)(c[i] >> (2 * W));
+      for (int u = 0; u <= TS / 4; ++u) zq[u] = *reinterpret_cast<const uint4*>(zb0 - 4 * u);
+      uint64_t acc[4] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-    for (int i = 0; i < NN; ++i) out[i] = t0 + i < K ? (lim[i + 1] & MASK) + (lim[i] >> W) : 0u;
-  }
-
-  // col += a x b (b in z, Z-padded; col zeroed, or holding T): HI adds the
-  // upper columns, TM bounds the terms of the main pairs (64 when only the
-  // low columns are wanted: lane l <= 63 has no low term beyond t = l). NA:
-  // a is given as lazy columns (a + G), reduced mod R on the fly (the limbs
-  // of T mod R and of m are never stored). Wave w takes terms [w S, (w+1) S)
-  // of pairs 0..63 (a is zero beyond K, and a zero a_t meets whatever z holds
-  // below its row); the extra pairs are cut into chunks of CH terms over all
-  // threads.
-  template <bool HI, int TM, bool NA>
-  static XHE_DEV void prod(const void* asrc, const uint32_t* z, uint64_t* col) {
-    constexpr int S = span(TM);
-    const int l = tid() & 63, t0 = __builtin_amdgcn_readfirstlane(tid() >> 6) * S;
-    uint32_t av[S];
-    if constexpr (NA) {
-      norm_range<S>(static_cast<const uint64_t*>(asrc), t0, av);
-    } else {
-      const uint32_t* ap = static_cast<const uint32_t*>(asrc) + t0;
+      for (int u = 0; u < TS / 4; ++u) {
+        const uint32_t zz[8] = {zq[u + 1].x, zq[u + 1].y, zq[u + 1].z, zq[u + 1].w,
+                                zq[u].x,     zq[u].y,     zq[u].z,     zq[u].w};  // Z[B_u - 4 + k]
+        const uint32_t at[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
 #pragma unroll
-      for (int r = 0; r < S; r += 4) {
-        const uint4 a4 = *reinterpret_cast<const uint4*>(ap + r);
-        av[r] = a4.x;
-        av[r + 1] = a4.y;
-        av[r + 2] = a4.z;
-        av[r + 3] = a4.w;
+        for (int r = 0; r < 4; ++r)  // column 4q + i, term t0 + 4u + r: Z[B_u + i - r]
+          mad4(acc, at[r], at[r], at[r], at[r], zz[4 - r], zz[5 - r], zz[6 - r], zz[7 - r]);
       }
-    }
-    uint64_t lo[4] = {0ull, 0ull, 0ull, 0ull}, hi[4] = {0ull, 0ull, 0ull, 0ull};
-    const uint32_t* zl = z + l - t0;
 #pragma unroll
-    for (int r = 0; r < S; r += 4) {
-      uint32_t zlo[4], zhi[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        zlo[q] = zl[K - r - q];
-        if constexpr (HI) zhi[q] = zl[2 * K - r - q];
-      }
-      mad4(lo, av[r], av[r + 1], av[r + 2], av[r + 3], zlo[0], zlo[1], zlo[2], zlo[3]);
-      if constexpr (HI) mad4(hi, av[r], av[r + 1], av[r + 2], av[r + 3], zhi[0], zhi[1], zhi[2], zhi[3]);
-    }
-    // chunk h of extra pair 64 + xi: terms h CH .. h CH + CH - 1
-    uint64_t elo = 0, ehi = 0;
-    const int xi = tid() / NCH, h = tid() - xi * NCH;
-    const bool xl = NX > 0 && xi < NX;
-    const int c = 64 + xi, c0 = h * CH;
-    if (xl) {
-      uint32_t ax[CH];
-      if constexpr (NA) {
-        norm_range<CH>(static_cast<const uint64_t*>(asrc), c0, ax);
-      } else {
-#pragma unroll
-        for (int q = 0; q < CH; ++q) ax[q] = static_cast<const uint32_t*>(asrc)[c0 + q];
-      }
-      const uint32_t* zp = z + (K + c - c0 - (CH - 1));
-#pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        elo = mad64(ax[q], zp[CH - 1 - q], elo);
-        if constexpr (HI) ehi = mad64(ax[q], zp[K + CH - 1 - q], ehi);
-      }
-    }
-    atomicAdd((unsigned long long*)&col[G + l], (unsigned long long)((lo[0] + lo[1]) + (lo[2] + lo[3])));
-    if constexpr (HI)
-      atomicAdd((unsigned long long*)&col[G + K + l], (unsigned long long)((hi[0] + hi[1]) + (hi[2] + hi[3])));
-    if (xl) {
-      atomicAdd((unsigned long long*)&col[G + c], (unsigned long long)elo);
-      if constexpr (HI) atomicAdd((unsigned long long*)&col[G + K + c], (unsigned long long)ehi);
+      for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long*)&col[G + 4 * q + i], (unsigned long long)acc[i]);
     }
     sync();
   }
 
-  // dst = U / R from the columns of U = T + m N (= 0 mod R); zeroes the
-  // other column buffer and mcol for the next product. The low part reduced
+  // dst = U / R from the columns of U = T + m N (= 0 mod R). The low part reduced
   // twice, L = sum v_j 2^(W j) (v_j <= MASK + 2), is 0 or R; if R then
   // v_(K-1) >= MASK - 1 (the limbs below sum to < 2^(W (K-1)) (1 + 3/MASK)),
   // else every v_j is 0: the carry out of the low part is v_(K-1) != 0, which
@@ -215,10 +165,8 @@ struct WaveMont {
       const uint32_t hp = i == 0 ? 0u : split3(cg, K + i - 1) + (i == 1 ? e0 : 0u);
       const uint32_t v = (hi & MASK) + (hp >> W);
       dst[i] = v;
-      if (zbw) s.zb[K + i] = v;
+      if (zbw) s.zb[ZO + i] = v;
     }
-    for (int j = tid(); j < 2 * K; j += NT) s.col[cur ^ 1][G + j] = 0ull;
-    for (int j = tid(); j < K; j += NT) s.mcol[G + j] = 0ull;
     sync();
   }
 
@@ -227,22 +175,29 @@ struct WaveMont {
     for (int j = tid(); j < K; j += NT) out[j] = norm(col + G, j);
     sync();
   }
+  // the same for T (the first pass of a product); the threads beyond K zero
+  // the other column buffer (last read by the previous product's tail, next
+  // written by the next product) and mcol (last read by the previous
+  // product, next written by this one's quotient product)
+  static XHE_DEV void norm_low_t(Lds& s, int cur) {
+    const int j = tid();
+    if (j < K) {
+      s.tl[j] = norm(s.col[cur] + G, j);
+    } else {
+      for (int i = j - K; i < 2 * K; i += NT - K) s.col[cur ^ 1][G + i] = 0ull;
+      for (int i = j - K; i < 4 * NQL; i += NT - K) s.mcol[G + i] = 0ull;
+    }
+    sync();
+  }
 
   // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N)
   static XHE_DEV void reduce(Lds& s, int cur, uint32_t* dst, bool zbw) {
-#if XHE_WAVE_FUSE
-    prod<false, 64, true>(s.col[cur] + G, s.znp, s.mcol);  // m = (T mod R) N' mod R
-    XHE_WAVE_T(1);
-    prod<true, K, true>(s.mcol + G, s.zn, s.col[cur]);     // U = T + m N
-    XHE_WAVE_T(2);
-#else
-    norm_low(s.col[cur], s.tl);
-    prod<false, 64, false>(s.tl, s.znp, s.mcol);  // m = (T mod R) N' mod R
+    norm_low_t(s, cur);
+    prodq<true>(s.tl, s.znp, s.mcol);  // m = (T mod R) N' mod R
     XHE_WAVE_T(1);
     norm_low(s.mcol, s.mq);
-    prod<true, K, false>(s.mq, s.zn, s.col[cur]);  // U = T + m N
+    prodq<false>(s.mq, s.zn, s.col[cur]);  // U = T + m N
     XHE_WAVE_T(2);
-#endif
     tail(s, cur, dst, zbw);
     XHE_WAVE_T(3);
   }
@@ -252,7 +207,7 @@ struct WaveMont {
   static XHE_DEV void mul(Lds& s, int& cur, const uint32_t* a, uint32_t* dst, bool zbw) {
     cur ^= 1;
     XHE_WAVE_T(-1);
-    prod<true, K, false>(a, s.zb, s.col[cur]);
+    prodq<false>(a, s.zb, s.col[cur]);
     XHE_WAVE_T(0);
     reduce(s, cur, dst, zbw);
   }
@@ -297,11 +252,12 @@ __global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_
   }
   WM::sync();
   for (int j = l; j < K; j += NT) {
-    s.zn[K + j] = md.N[j];
-    s.znp[K + j] = np[j];
+    s.zn[WM::ZO + j] = md.N[j];
+    s.znp[WM::ZO + j] = np[j];
     s.r3[j] = md.R3[j];
   }
   if (l == 0) s.one[0] = 1u;
+  for (int j = l; j < (ebits + 31) / 32 && j < 64; j += NT) s.exw[j] = ex[j];
   int cur = 0;
   {  // c (n2w words, < 2^(28 * 2K)) as 2K limbs in the columns
     const uint32_t* cw = c_words + (size_t)e * key.n2w;
@@ -319,7 +275,7 @@ __global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_
   auto bits64 = [&](int i, int& base) {
     const int wi = i >> 5;
     base = (wi - 1) * 32;
-    return ((uint64_t)ex[wi] << 32) | (wi > 0 ? ex[wi - 1] : 0u);
+    return ((uint64_t)s.exw[wi] << 32) | (wi > 0 ? s.exw[wi - 1] : 0u);
   };
   int i = ebits - 1;
   while (i >= 0 && !((ex[i >> 5] >> (i & 31)) & 1u)) --i;
@@ -360,7 +316,7 @@ __global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_
         for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
         if (step == 17) {  // the first window's odd power is the start value
           WM::copy_in(s.x, s.tab[val >> 1], K);
-          WM::copy_in(s.zb + K, s.tab[val >> 1], K);
+          WM::copy_in(s.zb + WM::ZO, s.tab[val >> 1], K);
           WM::sync();
           step = 18;
         } else {
