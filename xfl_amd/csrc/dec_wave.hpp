@@ -68,7 +68,7 @@ struct WaveMont {
   static constexpr int W = 28;
   static constexpr uint32_t MASK = (1u << W) - 1u;
   static constexpr int NT = 64 * NWV;  // threads per residue
-  static constexpr int TS = 16;
+  static constexpr int TS = NWV >= 8 ? 8 : 16;  // terms per slice
   static constexpr int NS = (K + TS - 1) / TS;
   static constexpr int NQF = (2 * K - 1 + 3) / 4, NQL = (K + 3) / 4;
   static_assert(NQF * NS <= NT, "one (quad, slice) per thread");
