@@ -113,18 +113,22 @@ def pick_window(bits, free_bytes, margin=16 << 30, split=False):
     return best[1] if best else 12
 
 
-def pmc_traffic(win_bits, n):
-    """HBM bytes per k_djn_pow launch from the committed rocprofv3 PMC passes
+def pmc_traffic(win_bits, n, kernel="k_djn_pmd"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/profile_box.sh -> tools/pmc_traffic.py), when they were taken on
     this configuration; else None. Counters cannot be read inside this run
-    (rocprofv3 --pmc is its own pass)."""
+    (rocprofv3 --pmc is its own pass). The newest round's file wins (the
+    kernel changed between rounds; before round 4 the files were named after
+    the k_djn_pow label)."""
     from xfl_amd._native import win_spec
-    for rnd in ("r3", "r2"):  # the newest round's passes (the kernel changed between rounds)
-        path = os.path.join(ROOT, "profiles", rnd, "k_djn_pow_pmc.json")
+    for rnd, name in (("r4", kernel), ("r3", "k_djn_pow"), ("r2", "k_djn_pow")):
+        path = os.path.join(ROOT, "profiles", rnd, f"{name}_pmc.json")
         try:
             with open(path) as f:
                 rec = json.load(f)
         except (OSError, ValueError):
+            continue
+        if rec.get("kernel", kernel) != kernel and rnd == "r4":
             continue
         if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
             return None, None
@@ -374,15 +378,33 @@ def headline_at_window(nat, L, bits, key_material, win, x, m, ex, st, rnd, N, st
     torch.cuda.synchronize()
     wall = time.time() - t0
     tot, cnt = ctypes.c_double(), ctypes.c_int64()
-    nat.check(L.xhe_profile_read(b"k_djn_pow", ctypes.byref(tot), ctypes.byref(cnt)))
+    kname = timed_kernel(L, tot, cnt)
     L.xhe_profile(0)
     _, w_pow = algorithmic_macs_per_element(bits, win, k.rand_bits)
     avg = tot.value / max(cnt.value, 1) / 1e3
     rec = {"window_bits": win, "value": N * steps / wall, "unit": "encrypts/s", "ms_per_step": wall / steps * 1e3,
-           "kernel_avg_ms": avg * 1e3, "frac": N * w_pow / avg / PEAK_MAC_PER_S,
+           "kernel": kname, "kernel_avg_ms": avg * 1e3, "frac": N * w_pow / avg / PEAK_MAC_PER_S,
            "table_bytes": nat.table_bytes(bits, win)}
     del k, ct
     return rec
+
+
+# the fixed-base encryption kernel per key size, as rocprof names it (the
+# library's hipEvent scopes carry the same labels): Montgomery digits at
+# 2048 (k_djn_pmd) and 3072/4096 (k_djn_pmdx), Montgomery rows through LDS or
+# the multi-lane Montgomery kernel otherwise
+DJN_KERNELS = ("k_djn_pmd", "k_djn_pmdx", "k_djn_pow_lds", "k_djn_pow")
+
+
+def timed_kernel(L, tot, cnt):
+    """Read the hipEvent totals of whichever DJN kernel ran; returns its name."""
+    import ctypes
+    from xfl_amd import _native as nat
+    for name in DJN_KERNELS:
+        nat.check(L.xhe_profile_read(name.encode(), ctypes.byref(tot), ctypes.byref(cnt)))
+        if cnt.value:
+            return name
+    return DJN_KERNELS[-1]
 
 
 def host_cores():
@@ -425,6 +447,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ops", action="store_true", help="skip the secondary-operation rates")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL process group and gather through it even at --gpus 1 (the N-GPU "
+                         "code path - init, async all-gather, barriers, max-over-ranks all-reduce - on one GPU)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -444,8 +469,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        if env_world is None:  # --dist at one GPU without a launcher: a group of one rank
+            from xfl_amd.shard import free_port
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
 
     bits = args.key_bits
     p, q, n, h = make_key(bits, seed=2024)
@@ -474,7 +504,7 @@ def main():
         nat.check(L.xhe_rand(dk.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
         nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
 
-    pipe = GatherPipeline(encrypt_shard, N, dk.n2w, world=world, rank=rank, device="cuda")
+    pipe = GatherPipeline(encrypt_shard, N, dk.n2w, world=world, rank=rank, device="cuda", collective=use_dist)
     last = 1_000_000 + max(args.warmup, 1) - 1  # the parity check below needs one finished step
     for i in range(1_000_000, last + 1):
         pipe.step(i)
@@ -490,10 +520,10 @@ def main():
     def expected(i):
         return O.encrypt_m(okey, O.encode_element(okey, float(xs[i]), 7)[0], nat.words_to_ints(rnd_h[i]))
 
-    parity_ok = shard_parity(pipe.shard(last), pipe.vector(last) if world > 1 else None, rank, idx, expected)
+    parity_ok = shard_parity(pipe.shard(last), pipe.vector(last) if use_dist else None, rank, idx, expected)
 
     L.xhe_profile(1)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -505,18 +535,17 @@ def main():
     pipe.drain()
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     wall = time.time() - t0
     ms_total = ev0.elapsed_time(ev1)
     import ctypes
     tot = ctypes.c_double()
     cnt = ctypes.c_int64()
-    kname = "k_djn_pow"
-    nat.check(L.xhe_profile_read(kname.encode(), ctypes.byref(tot), ctypes.byref(cnt)))
+    kname = timed_kernel(L, tot, cnt)
     L.xhe_profile(0)
     elapsed = max(wall, ms_total / 1e3)
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -529,17 +558,17 @@ def main():
         w_elem, w_pow = algorithmic_macs_per_element(bits, args.win, dk.rand_bits)
         pow_avg_s = (tot.value / max(cnt.value, 1)) / 1e3
         achieved = N * w_pow / pow_avg_s / 1e12  # N elements x 2 primes per launch
-        traffic, traffic_src = pmc_traffic(args.win, N)
+        traffic, traffic_src = pmc_traffic(args.win, N, kname) if bits == 2048 else (None, None)
         rec = {
             "metric": "2048-bit Paillier encrypts/s (device-resident)" if bits == 2048 else f"{bits}-bit Paillier encrypts/s (device-resident)",
             "value": value, "unit": "encrypts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"DJN private-key (CRT) encrypt, obfuscated, precision 7, {N} float64 "
-                                   f"plaintexts/GPU resident in HBM" + (", + RCCL all-gather" if world > 1 else ""),
+                                   f"plaintexts/GPU resident in HBM" + (", + RCCL all-gather" if use_dist else ""),
                        "key_bits": bits, "elements_per_gpu": N, "fixed_base_window_bits": args.win & 0xFF,
                        "fixed_base_window_split": bool(args.win & nat.XHE_WIN_SPLIT),
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world}" + ("+rccl" if use_dist else "")},
             "roofline": {"bound": "valu-int", "achieved": achieved, "peak": PEAK_MAC_PER_S / 1e12,
                          "unit": "TMAC/s", "frac": achieved * 1e12 / PEAK_MAC_PER_S, "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": kname, "kernel_avg_ms": pow_avg_s * 1e3,
@@ -565,7 +594,7 @@ def main():
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baselines(bits, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -198,3 +198,4 @@ def test_shifted_words_matches_python_ints():
         want = [int(a) << int(b) for a, b in zip(k, s)]
         assert words_to_ints(w) == want
         assert max(v.bit_length() for v in want) <= kbits
+

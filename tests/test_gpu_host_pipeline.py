@@ -192,7 +192,7 @@ def test_failing_chunk_leaves_pipeline_usable():
     import sys
 
     from tests.conftest import ROOT
-    env_ = dict(os.environ, XHE_TEST_FAIL_CHUNK="3")
+    env_ = dict(os.environ, XHE_TEST_HOOKS="1", XHE_TEST_FAIL_CHUNK="3")
     r = subprocess.run([sys.executable, "-c", _FAIL_SCRIPT.format(root=ROOT)], env=env_, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

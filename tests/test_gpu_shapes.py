@@ -167,3 +167,71 @@ def test_public_nodjn_encrypt_closed_form(fx):
     ct = nat.words_to_ints(dk.encrypt_words(nat.ints_to_words(ms, dk.nw), nat.ints_to_words(rs, dk.rand_words)))
     for i in list(range(4)) + [count // 2, count - 1]:
         assert ct[i] == (1 + n * ms[i]) * pow(rs[i], n, n2) % n2, i
+
+
+@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+def test_decrypt_digits_batch(fx):
+    """3072/4096-bit decrypt of batches above the 16-lane limit (5,120) runs in
+    Montgomery digits of P (k_p2_reduce_words, k_dec_pmdx_in/pow/out): the
+    round trip of 6,000 device encryptions is bit-exact, and arbitrary
+    residues mod n^2 (not ciphertexts) decrypt as the oracle's
+    L(c^(p-1) mod p^2) hp mod p with CRT (paillier.py:341-368)."""
+    from oracle import paillier_oracle as O
+    from xfl_amd import _native as nat
+    g = load_fixture(fx)
+    k = g["key"]
+    p, q, h = hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
+    n = p * q
+    dk = nat.DeviceKey(g["key_bits"], n, p, q, h, device=0, win_bits=10)
+    rng = random.Random(13)
+    count = 6000
+    ms = [rng.randrange(n) for _ in range(count)]
+    rs = [rng.randrange(1, 1 << dk.rand_bits) for _ in range(count)]
+    ct = dk.encrypt_words(nat.ints_to_words(ms, dk.nw), nat.ints_to_words(rs, dk.rand_words))
+    assert nat.words_to_ints(dk.decrypt_words(ct)) == ms
+    ok = O.derive_private(p, q, h)
+    cs = [rng.randrange(1, n * n) for _ in range(count)]
+    cs[:3] = [1, n * n - 1, n + 1]
+    got = nat.words_to_ints(dk.decrypt_words(nat.ints_to_words(cs, dk.n2w)))
+    for i in (0, 1, 2, 3, 2047, count - 1):
+        assert got[i] == O.decrypt_raw(ok, cs[i]), i
+
+
+_PIN_SCRIPT = r"""
+import sys
+sys.path.insert(0, {root!r})
+import torch
+torch.cuda.init()
+from tests.conftest import hx, load_fixture
+from xfl_amd import _native as nat
+g = load_fixture({fx!r})
+k = g["key"]
+p, q, h = hx(k["p"]), hx(k["q"]), hx(k["h_pow_n"])
+dk = nat.DeviceKey(g["key_bits"], p * q, p, q, h, device=0, win_bits=8)
+cts, want = [], []
+for case, enc in g["encrypt"].items():
+    if not isinstance(enc, dict) or case not in g["decrypt"]:
+        continue
+    dec = g["decrypt"][case]
+    cts += [hx(r) for r in enc["raw"]]
+    want += [hx(m) for m in dec["m"][len(dec["m"]) - len(enc["raw"]):]]
+got = nat.words_to_ints(dk.decrypt_words(nat.ints_to_words(cts, dk.n2w)))
+assert got == want, "golden decrypt differs"
+print("ok", len(got))
+"""
+
+
+@pytest.mark.parametrize("fx", ["paillier_3072_djn.json", "paillier_4096_djn.json"])
+def test_decrypt_digits_golden_pinned(fx):
+    """Every golden ciphertext of the 3072/4096-bit fixtures decrypts to the
+    reference's m through the digit kernels ($XHE_DEC_TPI=1 pins them for
+    small batches; the pin is read once per process, hence the child)."""
+    import os
+    import subprocess
+    import sys
+
+    from tests.conftest import ROOT
+    env_ = dict(os.environ, XHE_DEC_TPI="1")
+    r = subprocess.run([sys.executable, "-c", _PIN_SCRIPT.format(root=ROOT, fx=fx)], env=env_, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

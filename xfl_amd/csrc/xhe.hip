@@ -118,6 +118,17 @@ decltype(auto) with_shape(int K, F&& f) {
 }
 #endif
 
+#if XHE_NDIG
+// $XHE_NDIG_PUB=0: public DJN keys keep Montgomery n^2 tables (k_djn_pub; A/B)
+bool ndig_pub_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_NDIG_PUB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+#endif
+
 struct ModSpec {
   int S, W;
   int S4() const { return (S + 3) & ~3; }
@@ -143,11 +154,14 @@ struct Blob {
 };
 
 struct ModOff {
-  size_t N, R1, R2, R3;
+  size_t N, R1, R2, R3, Rpow = 0;
   uint32_t n0inv;
+  int npow = 0;
 };
 
-ModOff put_mod(Blob& bl, const BigU& M, const ModSpec& s) {
+// npow > 0 also stores R^j mod M for j < npow (consecutive rows of S4 limbs):
+// the fix-up factors of chains over plain residues (k_chunk_prod, raw inputs)
+ModOff put_mod(Blob& bl, const BigU& M, const ModSpec& s, int npow = 0) {
   ModOff o;
   BigU R = pow2((size_t)s.W * s.S);
   BigU R1 = mod(R, M);
@@ -158,6 +172,15 @@ ModOff put_mod(Blob& bl, const BigU& M, const ModSpec& s) {
   o.R2 = bl.put_limbs(R2, s);
   o.R3 = bl.put_limbs(R3, s);
   o.n0inv = mont_ninv(M.word(0), s.W);
+  if (npow > 0) {
+    BigU x = mod(BigU(1), M);
+    for (int j = 0; j < npow; ++j) {
+      const size_t off = bl.put_limbs(x, s);
+      if (j == 0) o.Rpow = off;
+      x = mulmod(x, R1, M);
+    }
+    o.npow = npow;
+  }
   return o;
 }
 
@@ -288,7 +311,7 @@ void build_tables_m(xhe_key* k, const ModDev& md, const uint32_t* d_hM, uint32_t
 }
 
 ModDev moddev(uint32_t* base, const ModOff& o) {
-  return ModDev{base + o.N, base + o.R1, base + o.R2, base + o.R3, o.n0inv};
+  return ModDev{base + o.N, base + o.R1, base + o.R2, base + o.R3, o.n0inv, o.npow ? base + o.Rpow : nullptr};
 }
 
 void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, const BigU* h, int win) {
@@ -303,8 +326,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   size_t o_maxpos = bl.put_words(maxpos, k->nw);
   size_t o_minneg = bl.put_words(minneg, k->nw);
   size_t o_nlim = bl.put_limbs(n, k->mp2);
-  ModOff o_n2m = put_mod(bl, n2, k->mn2);
-  ModOff o_n2X = put_mod(bl, n2, k->mn2X);
+  ModOff o_n2m = put_mod(bl, n2, k->mn2, kRpowRows);
+  ModOff o_n2X = put_mod(bl, n2, k->mn2X, kRpowRows);
   size_t o_nR2n2, o_hMn2 = 0;
   {
     BigU Rn2 = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
@@ -318,7 +341,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   // MASK + E_i with E = (1 - R) mod n
   struct {
     ModOff nd;
-    size_t kn2 = 0, rmn = 0, dw = 0, d1 = 0, topc = 0;
+    size_t kn2 = 0, rmn = 0, dw = 0, d1 = 0, topc = 0, dwt = 0;
   } on;
   if (K == 2048) {
     const ModSpec sn{80, 27};
@@ -345,6 +368,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     const BigU R2 = mulmod(mod(R, n2), mod(R, n2), n2);  // R^2 mod n^2
     on.d1 = digits(R2);                                   // 1 R^2
     on.dw = digits(mulmod(R2, R2, n2));                   // R^2 R^2
+    // R^2 R_MN2^-1 (R_MN2 = 2^(27*152), the public DJN tables' Montgomery
+    // factor): converts their rows to canonical digits (k_tab_to_pmdx, n)
+    const BigU RM = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
+    on.dwt = digits(mulmod(mulmod(R2, R2, n2), mulmod(R2, modinv(RM, n2), n2), n2));
     std::vector<uint32_t> tc = submod(BigU(1), Rn, n).to_limbs(27, 80);
     for (auto& x : tc) x += (1u << 27) - 1u;
     on.topc = bl.put(tc);
@@ -366,6 +393,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t nprime_p2 = 0, nprime_q2 = 0;
     ModOff xd[2];
     size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
+    size_t xdw[2] = {0, 0}, xhpR[2] = {0, 0};
   } o;
   int pm1_bits = 0, qm1_bits = 0, ep_bits = 0, eq_bits = 0;
   if (k->priv) {
@@ -460,11 +488,12 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     }
 #endif
 #if XHE_PMDX
-    if (k->djn && (K == 3072 || K == 4096)) {
-      // Montgomery digits mod P^2 over 4 lanes (k_djn_pmdx): per prime the
-      // modulus P in K limbs of 27 bits (R = 2^(27 K)), ceil(R/P) P^2, R - P,
-      // MASK + E_i, the fold constant Q R^3 mod P and the digits of
+    if (K == 3072 || K == 4096) {
+      // Montgomery digits mod P^2 over 4 lanes (k_djn_pmdx, k_dec_pmdx_*): per
+      // prime the modulus P in K limbs of 27 bits (R = 2^(27 K)), ceil(R/P)
+      // P^2, R - P, MASK + E_i, the fold constant Q R^3 mod P, the digits of
       // R^2 R_MP2^-1 mod P^2 (R_MP2: the MP2 shape's R, the tables' factor)
+      // and of R^2 mod P^2 (plain conversion), and hp R mod P (decrypt)
       const int KD = K == 3072 ? 60 : 80;
       const ModSpec sd{KD, 27};
       const BigU Rd = pow2((size_t)27 * KD), RM = pow2((size_t)s2.W * s2.S);
@@ -482,20 +511,26 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
         for (auto& x : tc) x += (1u << 27) - 1u;
         o.xtopc[i] = bl.put(tc);
         o.xfold[i] = bl.put_limbs(mulmod(mod(Y, X), mulmod(mulmod(RdX, RdX, X), RdX, X), X), sd);
-        // digits (e, f) of w = R^2 R_MP2^-1 mod X^2: R e + X f = w R^2 (mod X^2)
+        // digits (e, f) of w: R e + X f = w R^2 (mod X^2), as K interleaved pairs;
+        // Xw = w R^2 mod X^2
+        auto put_digits = [&](const BigU& Xw) {
+          const BigU e = mulmod(mod(Xw, X), modinv(RdX, X), X);
+          BigU Qd;
+          divmod(add(Xw, mul(Rd, sub(X, e))), X, &Qd, nullptr);
+          const BigU f = submod(mod(Qd, X), RdX, X);
+          const std::vector<uint32_t> el = e.to_limbs(27, KD), fl = f.to_limbs(27, KD);
+          std::vector<uint32_t> v(2 * KD);
+          for (int j = 0; j < KD; ++j) {
+            v[2 * j] = el[j];
+            v[2 * j + 1] = fl[j];
+          }
+          return bl.put(v);
+        };
         const BigU Rd2 = mulmod(mod(Rd, X2), mod(Rd, X2), X2);
-        const BigU Xw = mulmod(mulmod(Rd2, Rd2, X2), modinv(mod(RM, X2), X2), X2);
-        const BigU e = mulmod(mod(Xw, X), modinv(RdX, X), X);
-        BigU Qd;
-        divmod(add(Xw, mul(Rd, sub(X, e))), X, &Qd, nullptr);
-        const BigU f = submod(mod(Qd, X), RdX, X);
-        const std::vector<uint32_t> el = e.to_limbs(27, KD), fl = f.to_limbs(27, KD);
-        std::vector<uint32_t> v(2 * KD);
-        for (int j = 0; j < KD; ++j) {
-          v[2 * j] = el[j];
-          v[2 * j + 1] = fl[j];
-        }
-        o.xdwt[i] = bl.put(v);
+        const BigU Rd4 = mulmod(Rd2, Rd2, X2);
+        o.xdwt[i] = put_digits(mulmod(Rd4, modinv(mod(RM, X2), X2), X2));  // w = R^2 R_MP2^-1
+        o.xdw[i] = put_digits(Rd4);                                        // w = R^2
+        o.xhpR[i] = bl.put_limbs(mulmod(i ? hq : hp, RdX, X), sd);
       }
     }
 #endif
@@ -536,6 +571,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.nd_topc = B + on.topc;
     kd.nd_dw = reinterpret_cast<const uint2*>(B + on.dw);
     kd.nd_d1 = reinterpret_cast<const uint2*>(B + on.d1);
+    kd.nd_dwt = reinterpret_cast<const uint2*>(B + on.dwt);
   }
 #endif
   if (k->priv) {
@@ -587,7 +623,12 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     }
 #endif
 #if XHE_PMDX
-    if (k->djn && (K == 3072 || K == 4096)) {
+    if (K == 3072 || K == 4096) {
+      kd.pmdx_dec = 1;
+      kd.x_dw_p = reinterpret_cast<const uint2*>(B + o.xdw[0]);
+      kd.x_dw_q = reinterpret_cast<const uint2*>(B + o.xdw[1]);
+      kd.x_hpR_p = B + o.xhpR[0];
+      kd.x_hpR_q = B + o.xhpR[1];
       kd.dp = moddev(B, o.xd[0]);
       kd.dq = moddev(B, o.xd[1]);
       kd.x_kn2_p = B + o.xkn2[0];
@@ -672,6 +713,18 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       using Sh = decltype(sh);
       build_tables_sync<typename Sh::MN2, Sh::RW2>(k, &kd.n2, &hm, &tab, 1);
     });
+#if XHE_NDIG
+    if (K == 2048 && ndig_pub_on()) {
+      // rows as canonical Montgomery digits of n (e, f < n: 64 + 64 words,
+      // still 512 B) for k_djn_pub_nd
+      kd.pub_nd = 1;
+      using D = PMDX<80, 4>;
+      hipLaunchKernelGGL((k_tab_to_pmdx<D, 128>), dim3((unsigned)((rows * D::TPI + 127) / 128)), dim3(128), 0, nullptr,
+                         kd, 2, tab, (int64_t)rows, (int64_t)128);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipDeviceSynchronize());
+    }
+#endif
   }
 }
 
@@ -818,7 +871,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
 #if XHE_PMD && XHE_LDS_ROWS
     if constexpr (Sh::K == 2048) {
       if (k->kd.pmd) {
-        ProfScope ps("k_djn_pow", s);
+        ProfScope ps("k_djn_pmd", s);
         // small batches split each element's windows over G lanes (latency:
         // ~nwin/G + log2 G dependent products instead of nwin)
         const int G = pmd_split(n);
@@ -847,7 +900,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
         }
         const dim3 g4((unsigned)((n * D::TPI + 127) / 128), 2);
         {
-          ProfScope ps("k_djn_pow", s);
+          ProfScope ps("k_djn_pmdx", s);
           hipLaunchKernelGGL((k_djn_pmdx<D, Sh::RW>), g4, dim3(128), 0, s, k->kd, r + (size_t)off * k->rand_words,
                              k->rand_words, n, xst);
           HIPCHK(hipGetLastError());
@@ -871,7 +924,8 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
                          k->kd, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words, k->rand_words, n, ws);
       HIPCHK(hipGetLastError());
     } else {
-      ProfScope ps("k_djn_pow", s);
+      // labelled by the kernel rocprof shows (k_djn_pow_lds / k_djn_pow)
+      ProfScope ps(XHE_LDS_ROWS && MP2::TPI == 1 ? "k_djn_pow_lds" : "k_djn_pow", s);
 #if XHE_LDS_ROWS
       if constexpr (MP2::TPI == 1) {
 #if XHE_PQ_PAIR
@@ -908,6 +962,36 @@ int pow_grid(int64_t count, int cap_blocks) {
 template <class Sh>
 void encrypt_pub_djn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
                           hipStream_t s) {
+#if XHE_NDIG
+  if constexpr (Sh::K == 2048) {
+    if (k->kd.pub_nd) {
+      // fixed-base products in Montgomery digits of n (k_djn_pub_nd), then
+      // (1 + n m) folded in base n on the way out (k_ndig_out)
+      using D = PMDX<80, 4>;  // ND2048
+      const int64_t chunk = std::min<int64_t>(count, kChunk);
+      uint2* st = nullptr;
+      uint32_t* rows = nullptr;
+      ws_alloc((void**)&st, (size_t)D::K * chunk * sizeof(uint2), s);
+      ws_alloc((void**)&rows, (size_t)2 * D::MN::S4 * chunk * sizeof(uint32_t), s);
+      for (int64_t off = 0; off < count; off += chunk) {
+        const int64_t n = std::min(chunk, count - off);
+        const int eb = (int)((n * D::TPI + 127) / 128);
+        {
+          ProfScope ps("k_djn_pub", s);
+          hipLaunchKernelGGL((k_djn_pub_nd<D, Sh::RW2>), dim3(eb), dim3(128), 0, s, k->kd,
+                             r + (size_t)off * k->rand_words, k->rand_words, n, st);
+          HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL((k_ndig_out<D, true>), dim3(eb), dim3(128), 0, s, k->kd, st, m + (size_t)off * k->nw, n,
+                           ct + (size_t)off * k->n2w, rows);
+        HIPCHK(hipGetLastError());
+      }
+      ws_free(st, s);
+      ws_free(rows, s);
+      return;
+    }
+  }
+#endif
   using MN2 = typename Sh::MN2;
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
@@ -962,9 +1046,68 @@ void ndig_run(int64_t count, hipStream_t s, IN&& in, POW&& pw, OUT&& out) {
 }
 #endif
 
+#if XHE_PMD && XHE_LDS_ROWS
+// $XHE_NODJN_PMD=0: the Montgomery k_nodjn_crt instead (A/B measurement)
+bool nodjn_pmd_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_NODJN_PMD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Private non-DJN encryption of 2048-bit keys in Montgomery digits: r mod
+// P^2 -> digits (k_dec_pmd_in), r^(e_P) by the decrypt's digit
+// exponentiation (k_dec_pmd_pow, the exponent e_P = n mod phi(P^2) shared by
+// every lane), (1 + n m) folded in on the way out (k_nodjn_pmd_out), CRT.
+template <class Sh>
+void encrypt_nodjn_pmd(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
+                       hipStream_t s) {
+  using MP2 = typename Sh::MP2;
+  constexpr int NQ = PMD<37>::NQ;
+  const int64_t chunk = std::min<int64_t>(count, kChunk);
+  const int pow_blocks = (int)std::min<int64_t>((chunk + 127) / 128, 1024);
+  const int64_t lanes = (int64_t)pow_blocks * 128;
+  uint4 *ws = nullptr, *st = nullptr;
+  uint32_t* rows = nullptr;
+  ws_alloc((void**)&ws, (size_t)2 * 16 * NQ * lanes * sizeof(uint4), s);
+  ws_alloc((void**)&st, (size_t)2 * NQ * chunk * sizeof(uint4), s);
+  ws_alloc((void**)&rows, (size_t)2 * 2 * MP2::S4 * chunk * sizeof(uint32_t), s);
+  for (int64_t off = 0; off < count; off += chunk) {
+    const int64_t n = std::min(chunk, count - off);
+    const dim3 g1((unsigned)((n + 127) / 128), 2);
+    hipLaunchKernelGGL((k_dec_pmd_in<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                       k->kd.q2.N, r + (size_t)off * k->rand_words, k->rand_words, n, st);
+    HIPCHK(hipGetLastError());
+    {
+      ProfScope ps("k_nodjn_crt", s);
+      hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3((unsigned)std::min<int64_t>((n + 127) / 128, pow_blocks), 2),
+                         dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.ep_words, k->kd.ep_bits, k->kd.eq_words,
+                         k->kd.eq_bits, n, st, ws);
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_nodjn_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                       k->kd.q2.N, m + (size_t)off * k->nw, n, st, rows);
+    HIPCHK(hipGetLastError());
+    crt_enc_launch<Sh>(k, n, rows, ct + (size_t)off * k->n2w, s);
+  }
+  ws_free(ws, s);
+  ws_free(st, s);
+  ws_free(rows, s);
+}
+#endif
+
 template <class Sh>
 void encrypt_nodjn_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_t count, uint32_t* ct,
                         hipStream_t s) {
+#if XHE_PMD && XHE_LDS_ROWS
+  if constexpr (Sh::K == 2048) {
+    if (k->priv && nodjn_pmd_on()) {
+      encrypt_nodjn_pmd<Sh>(k, m, r, count, ct, s);
+      return;
+    }
+  }
+#endif
   if (k->priv) {
     using MP2 = typename Sh::MP2;
     // 2-lane batch shapes (3072 bits, 55 limbs per lane) spill in this
@@ -1170,14 +1313,17 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   return XHE_OK;
 }
 
-// Reduce segment-ordered Montgomery rows [S4][count] to one row per segment
-// (seg: nseg+1 offsets) by levels of k_chunk_prod (C rows per chunk). Takes
-// ownership of `rows`; returns a new [S4][nseg] buffer (hipFree by the
-// caller); an empty segment yields the Montgomery one.
+// Reduce segment-ordered rows [S4][count] to one Montgomery row per segment
+// (seg: nseg+1 offsets) by levels of k_chunk_prod (C rows per chunk). The
+// input rows are Montgomery rows, or plain residues with raw = true (the
+// first level then returns each chunk to Montgomery form). Takes ownership
+// of `rows`; returns a new [S4][nseg] buffer (hipFree by the caller); an
+// empty segment yields the Montgomery one.
 template <class Sh, class MN2 = typename Sh::MN2>
-uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s) {
+uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s,
+                          bool raw = false) {
   const int S4 = MN2::S4;
-  const int64_t C = 32;  // chunk length per level
+  const int64_t C = kRawChunk;  // chunk length per level
   const int64_t nseg = (int64_t)seg.size() - 1;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
   int64_t n_cur = count;
@@ -1201,7 +1347,8 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
     HIPCHK(hipMemcpyAsync(dcb, cb.data(), cb.size() * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(n_out, 1) * 4, s));
     hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, n_cur, dcb, n_out,
-                       nxt);
+                       nxt, raw ? 1 : 0);
+    raw = false;  // every later level multiplies Montgomery rows
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));  // cb lives on the host stack
     (void)hipFree(dcb);
@@ -1229,7 +1376,8 @@ void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dma
                        rows, sq);
     HIPCHK(hipGetLastError());
   }
-  uint32_t* cur = reduce_segments<Sh, MN2>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s);
+  uint32_t* cur =
+      reduce_segments<Sh, MN2>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s, true);
   hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, nseg, out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
@@ -1362,12 +1510,12 @@ void dec_pmd_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
   ws_alloc((void**)&st, (size_t)2 * NQ * chunk * sizeof(uint4), s);
   const dim3 g1((unsigned)((n + 127) / 128), 2);
   hipLaunchKernelGGL((k_dec_pmd_in<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
-                     k->kd.q2.N, ct, n, st);
+                     k->kd.q2.N, ct, k->n2w, n, st);
   HIPCHK(hipGetLastError());
   {
     ProfScope ps("k_dec_pow", s);
-    hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3(pow_blocks, 2), dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, n, st,
-                       ws);
+    hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3(pow_blocks, 2), dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N,
+                       k->kd.pm1_words, k->kd.pm1_bits, k->kd.qm1_words, k->kd.qm1_bits, n, st, ws);
     HIPCHK(hipGetLastError());
   }
   hipLaunchKernelGGL((k_dec_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
@@ -1375,6 +1523,60 @@ void dec_pmd_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
   HIPCHK(hipGetLastError());
   ws_free(ws, s);
   ws_free(st, s);
+}
+#endif
+
+#if XHE_PMDX
+// $XHE_DEC_PMDX=0: the Montgomery decrypt shapes instead (A/B measurement)
+bool dec_pmdx_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_DEC_PMDX");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// 3072/4096-bit decrypt in Montgomery digits up to m_P (k_dec_pmdx_*, see
+// xhe_kernels.hpp): writes mrows [prime][2 S4][count] as k_dec_fin does
+template <class Sh>
+void dec_pmdx_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chunk, uint32_t* mrows,
+                     hipStream_t s) {
+  using DO = typename Sh::PDXO;  // conversions (register room)
+  using DP = typename Sh::PDX;   // the exponentiation
+  using MP2L = typename Sh::MP2L;
+  using MP = typename Sh::MP;
+  constexpr int RW = Sh::RW, NWH = Sh::K / 64;
+  constexpr int SCR = MP2L::S4 > DO::MN::S4 ? MP2L::S4 : DO::MN::S4;
+  constexpr int GPB = 128 / DP::TPI;
+  const int pow_blocks = (int)std::min<int64_t>((chunk + GPB - 1) / GPB, 1024);
+  const int64_t gs = (int64_t)pow_blocks * GPB;
+  uint32_t *words = nullptr, *scr = nullptr;
+  uint2 *st = nullptr, *tab = nullptr;
+  ws_alloc((void**)&words, (size_t)2 * chunk * RW * sizeof(uint32_t), s);
+  ws_alloc((void**)&scr, (size_t)2 * SCR * chunk * sizeof(uint32_t), s);
+  ws_alloc((void**)&st, (size_t)2 * DP::K * chunk * sizeof(uint2), s);
+  ws_alloc((void**)&tab, (size_t)2 * 16 * DP::K * gs * sizeof(uint2), s);
+  hipLaunchKernelGGL((k_p2_reduce_words<MP2L, RW>), dim3((unsigned)((n * MP2L::TPI + 255) / 256), 2), dim3(256), 0, s,
+                     k->kd, ct, n, scr, words);
+  HIPCHK(hipGetLastError());
+  const dim3 go((unsigned)((n * DO::TPI + 127) / 128), 2);
+  hipLaunchKernelGGL((k_dec_pmdx_in<DO, RW>), go, dim3(128), 0, s, k->kd, words, n, st);
+  HIPCHK(hipGetLastError());
+  {
+    ProfScope ps("k_dec_pow", s);
+    const int pb = (int)std::min<int64_t>((n + GPB - 1) / GPB, pow_blocks);
+    hipLaunchKernelGGL(k_dec_pmdx_pow<DP>, dim3(pb, 2), dim3(128), 0, s, k->kd, n, st, tab);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL((k_dec_pmdx_out<DO, NWH>), go, dim3(128), 0, s, k->kd, n, st, scr, words);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_words_to_rows<MP>, dim3((unsigned)((n * MP::TPI + 255) / 256), 2), dim3(256), 0, s, words,
+                     NWH, n, mrows);
+  HIPCHK(hipGetLastError());
+  ws_free(words, s);
+  ws_free(scr, s);
+  ws_free(st, s);
+  ws_free(tab, s);
 }
 #endif
 
@@ -1399,6 +1601,19 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
   for (int64_t off = 0; off < count; off += chunk) {
     int64_t n = std::min(chunk, count - off);
     const uint32_t* cto = ct + (size_t)off * k->n2w;
+#if XHE_PMDX
+    if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+      if (k->kd.pmdx_dec && dec_pmdx_on() && (pin ? pin == 1 : tpi == 4)) {
+        // batches: digits (the 16-lane shape keeps the small ones)
+        dec_pmdx_launch<Sh>(k, cto, n, chunk, mrows, s);
+        const int cblocks = (int)((n * MP::TPI + 255) / 256);
+        hipLaunchKernelGGL(k_crt_dec<MP>, dim3(cblocks), dim3(256), 0, s, k->kd, k->kd.p.N, n, mrows,
+                           m + (size_t)off * k->nw);
+        HIPCHK(hipGetLastError());
+        continue;
+      }
+    }
+#endif
     if (tpi == 64) {
       if constexpr (wave_ok) {
         static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave shares the MP2 limbs");
@@ -1664,9 +1879,12 @@ int host_pipeline(const xhe_key* key, int64_t count, int64_t chunk, const std::v
       for (auto& x : s) (void)hipStreamSynchronize(x->s);
     }
   } drain{st_};
-  static const int64_t fail_chunk = [] {  // test hook: run() of this chunk fails (error-path tests)
+  // test hook: run() of this chunk fails (error-path tests). Armed only when
+  // XHE_TEST_HOOKS=1 is set as well, so a stray variable cannot fail a call.
+  static const int64_t fail_chunk = [] {
+    const char* on = getenv("XHE_TEST_HOOKS");
     const char* e = getenv("XHE_TEST_FAIL_CHUNK");
-    return e ? (int64_t)atoll(e) : (int64_t)-1;
+    return (on && on[0] == '1' && e) ? (int64_t)atoll(e) : (int64_t)-1;
   }();
   auto dptr = [&](int b, int k) { return dev[(size_t)b * parts.size() + k]->p; };
   auto enqueue = [&](int64_t c) -> int {
@@ -1973,7 +2191,9 @@ int xhe_mulmod(const xhe_key* key, const uint32_t* a_dev, const int32_t* ea_dev,
       using Sh = decltype(sh);
       if (row) mulmod_impl<Sh, typename Sh::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
       else mulmod_impl<Sh>(key, a_dev, ea_dev, b_dev, eb_dev, count, dmax, out_dev, eout_dev, hs);
-      if (ea_dev && eb_dev && dmax >= key->dneg)
+      // a NULL exponent array means all exponents 0 (include/xhe.h), so one
+      // array alone can still carry a gap >= dneg
+      if ((ea_dev || eb_dev) && dmax >= key->dneg)
         return row ? mulmod_gap_fix<Sh, typename Sh::MN2X>(key, a_dev, ea_dev, b_dev, eb_dev, count, out_dev, hs)
                    : mulmod_gap_fix<Sh, typename Sh::MN2>(key, a_dev, ea_dev, b_dev, eb_dev, count, out_dev, hs);
       return XHE_OK;

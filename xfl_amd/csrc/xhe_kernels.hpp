@@ -19,7 +19,14 @@ struct ModDev {
   const uint32_t* R2;  // R^2 mod N
   const uint32_t* R3;  // R^3 mod N
   uint32_t n0inv;
+  const uint32_t* Rpow;  // n^2 shapes: R^j mod N for j < kRpowRows, rows of S4 limbs (else null)
 };
+
+// Segment chunks of plain (non-Montgomery) residues are at most kRawChunk
+// long; such a chunk's product comes back to Montgomery form by one product
+// with R^(len + 1), so R^j is kept for j <= kRawChunk + 1.
+constexpr int kRawChunk = 32;
+constexpr int kRpowRows = kRawChunk + 2;
 
 // All pointers are device pointers into the key blob. Limb rows are padded to
 // a multiple of 4 words and 16-byte aligned.
@@ -83,6 +90,8 @@ struct KeyDev {
   ModDev nd;
   const uint32_t *nd_kn2, *nd_rmn, *nd_topc;
   const uint2 *nd_dw, *nd_d1;
+  const uint2* nd_dwt;  // digits of R^2 R_MN2^-1 (public DJN table rows -> digits)
+  int pub_nd;           // public DJN tables hold digits of n (k_djn_pub_nd)
   // ---- Montgomery digits mod P^2 over 4 lanes (PMDX, 3072/4096-bit DJN
   // private keys; k_djn_pmdx): P as K limbs of 27 bits, ceil(R/P) P^2, R - P,
   // MASK + E_i, the fold constant Q R^3 mod P (Q the other prime) and the
@@ -91,6 +100,11 @@ struct KeyDev {
   ModDev dp, dq;
   const uint32_t *x_kn2_p, *x_kn2_q, *x_rmn_p, *x_rmn_q, *x_topc_p, *x_topc_q, *x_fold_p, *x_fold_q;
   const uint2 *x_dwt_p, *x_dwt_q;
+  // the same digits for the decrypt of every 3072/4096-bit private key
+  // (k_dec_pmdx_*): the digits of R^2 mod P^2 and hp R mod P (27-bit limbs)
+  int pmdx_dec;
+  const uint2 *x_dw_p, *x_dw_q;
+  const uint32_t *x_hpR_p, *x_hpR_q;
   // ---- one-wave decrypt exponentiation (k_dec_wave, 2048-bit keys): the
   // full Montgomery inverse -P^-2 mod R of the MP2 shape (R = 2^(28*74))
   const uint32_t *p2_nprime, *q2_nprime;
@@ -841,15 +855,18 @@ XHE_DEV void pmd_pow_uniform(const PMD<KP>& M, uint32_t (&a)[KP], uint32_t (&c)[
 template <class D>
 struct PmdxKey {
   const ModDev& md;
-  const uint32_t *kn2, *rmn, *topc, *fold;
-  const uint2* dwt;
+  const uint32_t *kn2, *rmn, *topc, *fold, *hpR;
+  const uint2 *dwt, *dw;
+  // prime 0: p, 1: q, 2: n (the digits mod n^2 of k_ndig_*; public DJN tables)
   XHE_DEV PmdxKey(const KeyDev& k, int prime)
-      : md(prime ? k.dq : k.dp),
-        kn2(prime ? k.x_kn2_q : k.x_kn2_p),
-        rmn(prime ? k.x_rmn_q : k.x_rmn_p),
-        topc(prime ? k.x_topc_q : k.x_topc_p),
-        fold(prime ? k.x_fold_q : k.x_fold_p),
-        dwt(prime ? k.x_dwt_q : k.x_dwt_p) {}
+      : md(prime == 2 ? k.nd : prime ? k.dq : k.dp),
+        kn2(prime == 2 ? k.nd_kn2 : prime ? k.x_kn2_q : k.x_kn2_p),
+        rmn(prime == 2 ? k.nd_rmn : prime ? k.x_rmn_q : k.x_rmn_p),
+        topc(prime == 2 ? k.nd_topc : prime ? k.x_topc_q : k.x_topc_p),
+        fold(prime == 2 ? nullptr : prime ? k.x_fold_q : k.x_fold_p),
+        hpR(prime == 2 ? nullptr : prime ? k.x_hpR_q : k.x_hpR_p),
+        dwt(prime == 2 ? k.nd_dwt : prime ? k.x_dwt_q : k.x_dwt_p),
+        dw(prime == 2 ? k.nd_dw : prime ? k.x_dw_q : k.x_dw_p) {}
 };
 
 template <class D, int RW>
@@ -940,6 +957,123 @@ __global__ void __launch_bounds__(128, 2) k_pmdx_enc_out(KeyDev key, const uint3
   X.M.wide_mul_add_store(y1, ARow{pk.md.N}, rows, cnt, words + ((size_t)prime * count + e) * RW, RW);
 }
 
+// ---- Decryption of 3072/4096-bit keys in Montgomery digits (PMDX; as
+// k_dec_pmd_* for 2048): c mod P^2 as words (k_p2_reduce_words, the 4-lane
+// Montgomery shape), its digits (k_dec_pmdx_in), x = c^(P-1) by the
+// wave-uniform sliding window in digits (k_dec_pmdx_pow), and on the way out
+// (k_dec_pmdx_out) from_digits gives x = y0 + P y1 with y0 = x mod P = 1, so
+// L_P(x) = (x - 1) / P = y1 exactly and m_P = y1 hp mod P is one product
+// (paillier.py:341-368, context.py:190-194). m_P words -> MP rows
+// (k_words_to_rows) -> k_crt_dec.
+template <class MP2L, int RW>
+__global__ void __launch_bounds__(256, 2) k_p2_reduce_words(KeyDev key, const uint32_t* __restrict__ c_words,
+                                                            int64_t count, uint32_t* __restrict__ scr,
+                                                            uint32_t* __restrict__ words) {
+  const int prime = blockIdx.y;
+  const ModDev& md = prime ? key.q2L : key.p2L;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MP2L::TPI;
+  if (e >= count) return;
+  const int st = (int)count;
+  uint32_t* sq = scr + (size_t)prime * MP2L::S4 * count + e;
+  const int n2w = key.n2w;
+  const uint32_t* cw = c_words + (size_t)e * n2w;
+  MP2L M;
+  M.init(md.N, md.n0inv);
+  uint32_t b[MP2L::L];
+  {  // high limbs [S, 2S) of c into the scratch row (the REDC's upper half)
+    const int g = MP2L::G::g();
+#pragma unroll
+    for (int j = 0; j < MP2L::L; ++j) {
+      const int J = MP2L::S + g * MP2L::L + j;
+      const int bit = MP2L::W * J, k = bit >> 5, sh = bit & 31;
+      const uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+      sq[(size_t)(g * MP2L::L + j) * st] = (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2L::MASK;
+    }
+    if (g == 0)
+      for (int j = MP2L::S; j < MP2L::S4; ++j) sq[(size_t)j * st] = 0u;
+  }
+  M.load_words(b, cw, n2w);  // low S limbs
+  wave_sync_mem_();
+  M.redc_wide(b, AStrided{sq, st});  // c R^-1 mod P^2
+  M.mul(b, ARow{md.R2});             // c mod P^2
+  M.reduce_once(b);
+  wave_sync_mem_();
+  store_packed(M, b, sq, st, words + ((size_t)prime * count + e) * RW, RW);
+}
+
+template <class D, int RW>
+__global__ void __launch_bounds__(128, 2) k_dec_pmdx_in(KeyDev key, const uint32_t* __restrict__ words,
+                                                        int64_t count, uint2* __restrict__ st) {
+  constexpr int L = D::L;
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  const int prime = blockIdx.y;
+  const PmdxKey<D> pk(key, prime);
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = pk.topc[i];
+  __syncthreads();
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  D X;
+  X.init(pk.md.N, pk.md.n0inv);
+  uint32_t lo[L], hi[L], a[L], c[L];
+  const uint32_t* xe = words + ((size_t)prime * count + e) * RW;
+  pmdx_load<D, 0>(lo, xe, RW, g);
+  pmdx_load<D, D::K>(hi, xe, RW, g);
+  pmdx_to_digits(X, lo, hi, pk.kn2, pk.rmn, pk.dw, topc, a, c);
+  ndig_st_store<D>(a, c, st + (size_t)prime * D::K * count, count, e);
+}
+
+// st <- st^(P-1) per prime; tab: 16 digit states per group slot and prime
+template <class D>
+__global__ void __launch_bounds__(128, 2) k_dec_pmdx_pow(KeyDev key, int64_t count, uint2* __restrict__ st,
+                                                         uint2* __restrict__ ws) {
+  constexpr int GPB = 128 / D::TPI, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  const int prime = blockIdx.y;
+  const PmdxKey<D> pk(key, prime);
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = pk.topc[i];
+  __syncthreads();
+  const int gs = (int)gridDim.x * GPB;
+  const int gid0 = (int)blockIdx.x * GPB + (int)threadIdx.x / D::TPI;
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  uint2* tab = ws + (size_t)prime * 16 * D::K * gs + gid0;
+  uint2* stp = st + (size_t)prime * D::K * count;
+  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
+  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
+  for (int64_t e = gid0; e < count; e += gs) {
+    D X;
+    X.init(pk.md.N, pk.md.n0inv);
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, stp, count, e);
+    pmdx_pow_uniform(X, a, c, ex, ebits, tab, gs, ops, GPB, topc);
+    ndig_st_store<D>(a, c, stp, count, e);
+  }
+}
+
+// digits of x = c^(P-1) -> m_P = L_P(x) hp mod P as NWH words ([prime][count][NWH])
+template <class D, int NWH>
+__global__ void __launch_bounds__(128, 2) k_dec_pmdx_out(KeyDev key, int64_t count, const uint2* __restrict__ st,
+                                                         uint32_t* __restrict__ scr, uint32_t* __restrict__ words) {
+  constexpr int L = D::L;
+  const int prime = blockIdx.y;
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const PmdxKey<D> pk(key, prime);
+  D X;
+  X.init(pk.md.N, pk.md.n0inv);
+  uint32_t y0[L], y1[L];
+  {
+    uint32_t a[L], c[L];
+    ndig_st_load<D>(a, c, st + (size_t)prime * D::K * count, count, e);
+    pmdx_from_digits(X, a, c, y0, y1);
+  }
+  X.M.mul(y1, ARow{pk.hpR});  // L_P(x) hp mod P (< 2P)
+  X.M.reduce_once(y1);
+  store_packed(X.M, y1, scr + (size_t)prime * D::MN::S4 * count + e, (int)count,
+               words + ((size_t)prime * count + e) * NWH, NWH);
+}
+
 // c_P words [prime][count][nwords] -> the MP2 rows of k_crt_enc ([prime][2 S4][count])
 template <class MP2>
 __global__ void __launch_bounds__(256, 2) k_words_to_rows(const uint32_t* __restrict__ words, int nwords,
@@ -1013,13 +1147,16 @@ __global__ void __launch_bounds__(128, 2) k_tab_to_pmdx(KeyDev key, int prime, u
 // and one Montgomery product by 1; X_P = x - 1 written to xrows
 // [prime][xs4][count] exactly as k_dec_pow<MP2, 0>). The digit state between
 // them: st [prime][NQ quads][count] uint4 (interleaved limb pairs).
+// k_dec_pmd_in and k_dec_pmd_pow also serve the private non-DJN encryption
+// (r mod P^2 -> digits, r^(e_P); k_nodjn_pmd_out finishes it): c_words holds
+// nwords words per element (a ciphertext, or a draw r < n).
 template <class MP2, int KP>
 __global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_t* __restrict__ Pp,
                                                        const uint32_t* __restrict__ Pq,
                                                        const uint32_t* __restrict__ Np2,
                                                        const uint32_t* __restrict__ Nq2,
-                                                       const uint32_t* __restrict__ c_words, int64_t count,
-                                                       uint4* __restrict__ st) {
+                                                       const uint32_t* __restrict__ c_words, int nwords,
+                                                       int64_t count, uint4* __restrict__ st) {
   static_assert(MP2::TPI == 1 && MP2::S == 2 * KP && MP2::W == 28, "digits of the one-lane P^2 shape");
   constexpr int NQ = PMD<KP>::NQ;
   __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
@@ -1028,7 +1165,7 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_
   if (e >= count) return;
   const ModDev& md = prime ? key.q2 : key.p2;
   uint32_t* slot = img_all[(threadIdx.x >> 6) & 1] + (threadIdx.x & 63) * 4;
-  const int n2w = key.n2w;
+  const int n2w = nwords;
   const uint32_t* cw = c_words + (size_t)e * n2w;
   uint32_t x[MP2::L];
   {
@@ -1062,9 +1199,13 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_
                                        2 * q + 1 < KP ? a[2 * q + 1] : 0u, 2 * q + 1 < KP ? c[2 * q + 1] : 0u);
 }
 
+// st <- st^E_P per prime: E = P - 1 (decrypt) or e_P = n mod phi(P^2)
+// (private non-DJN obfuscator, paillier.py:214-227)
 template <int KP>
 __global__ void __launch_bounds__(128, 2) k_dec_pmd_pow(KeyDev key, const uint32_t* __restrict__ Pp,
-                                                        const uint32_t* __restrict__ Pq, int64_t count,
+                                                        const uint32_t* __restrict__ Pq,
+                                                        const uint32_t* __restrict__ ex_p, int bits_p,
+                                                        const uint32_t* __restrict__ ex_q, int bits_q, int64_t count,
                                                         uint4* __restrict__ st, uint4* __restrict__ ws) {
   using D = PMD<KP>;
   constexpr int NQ = D::NQ;
@@ -1074,8 +1215,8 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_pow(KeyDev key, const uint32
   const uint32_t* tcg = prime ? key.topc_q : key.topc_p;
   if (threadIdx.x < KP) topc[threadIdx.x] = tcg[threadIdx.x];
   __syncthreads();
-  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
-  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
+  const uint32_t* ex = prime ? ex_q : ex_p;
+  const int ebits = prime ? bits_q : bits_p;
   // 32-bit indices (count < 2^31 per launch), per-lane addresses formed at
   // use: the product needs every register it can get
   const int G = (int)(gridDim.x * blockDim.x);
@@ -1156,6 +1297,54 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_out(KeyDev key, const uint32
     br = x[j] < br ? 1u : 0u;
     xo[(size_t)j * count] = v & MP2::MASK;
   }
+}
+
+// Private non-DJN encryption, last step: (1 + n m) r^(e_P) mod P^2 from the
+// digits of r^(e_P) (k_dec_pmd_pow), as k_djn_pmd finishes: R a + P c is the
+// 74-limb Montgomery form, and the product with the plain 1 + n m leaves it.
+// Rows as k_crt_enc reads them ([prime][2 S4][count]).
+template <class MP2, int KP>
+__global__ void __launch_bounds__(128, 2) k_nodjn_pmd_out(KeyDev key, const uint32_t* __restrict__ Pp,
+                                                          const uint32_t* __restrict__ Pq,
+                                                          const uint32_t* __restrict__ Np2,
+                                                          const uint32_t* __restrict__ Nq2,
+                                                          const uint32_t* __restrict__ m_words, int64_t count,
+                                                          const uint4* __restrict__ st, uint32_t* __restrict__ rows) {
+  constexpr int NQ = PMD<KP>::NQ;
+  const int prime = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
+  uint32_t* slot = img_all[(threadIdx.x >> 6) & 1] + (threadIdx.x & 63) * 4;
+  {
+    const uint4* se = st + (size_t)prime * NQ * count + e;
+    uint32_t a[KP], c[KP], x[2 * KP];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint4 v = se[(size_t)q * count];
+      if (2 * q < KP) a[2 * q] = v.x, c[2 * q] = v.y;
+      if (2 * q + 1 < KP) a[2 * q + 1] = v.z, c[2 * q + 1] = v.w;
+    }
+    PMD<KP> M;
+    M.init(prime ? Pq : Pp, prime ? key.q.n0inv : key.p.n0inv);
+    M.to_mont2(a, c, x);  // r^e R^2 mod P^2, unreduced (< 2^13 P^2)
+#pragma unroll
+    for (int q = 0; q < MP2::S4 / 4; ++q)
+      *reinterpret_cast<uint4*>(slot + q * 256) =
+          make_uint4(4 * q < 2 * KP ? x[4 * q] : 0u, 4 * q + 1 < 2 * KP ? x[4 * q + 1] : 0u,
+                     4 * q + 2 < 2 * KP ? x[4 * q + 2] : 0u, 4 * q + 3 < 2 * KP ? x[4 * q + 3] : 0u);
+  }
+  wave_sync_mem_();
+  __builtin_amdgcn_sched_barrier(0);
+  MP2 N;
+  N.init(prime ? Nq2 : Np2, prime ? key.q2.n0inv : key.p2.n0inv);
+  uint32_t b[MP2::L];
+  N.load_words(b, m_words + (size_t)e * key.nw, key.nw);
+  N.mul(b, ARow{prime ? key.nR_q2 : key.nR_p2});  // n m mod P^2 (< 2 P^2), plain
+  b[0] += 1u;                                     // 1 + n m
+  N.mul(b, ALdsQ{slot});                          // (1 + n m) r^e mod P^2
+  N.reduce_once(b);
+  N.store_strided(b, rows + (size_t)prime * 2 * MP2::S4 * count + e, (int)count);
 }
 
 // Rewrite packed fixed-base table rows X = x R^2 mod P^2 (the 74-limb
@@ -1617,31 +1806,29 @@ __global__ void __launch_bounds__(256, 2) k_mulmod_n2(KeyDev key, const uint32_t
   M.init(Nn2, n2dev<MN2>(key).n0inv);
   const int e1 = ea ? ea[e] : 0, e2 = eb ? eb[e] : 0;
   const int emin = e1 < e2 ? e1 : e2;
-  const int d1 = e1 - emin, d2 = e2 - emin;
+  // x = the operand to align (larger exponent; a when equal), y = the other:
+  // MontMul(x^(2^d) R, y) = x^(2^d) y, so only x enters Montgomery form and
+  // the product leaves it by itself - 2 + d products (was 4 + d: both
+  // operands converted, then a product by 1)
+  const bool xb = e2 > e1;
+  const int dx = (xb ? e2 : e1) - emin;
+  const uint32_t* xw = (xb ? bw : a) + (size_t)e * key.n2w;
+  const uint32_t* yw = (xb ? a : bw) + (size_t)e * key.n2w;
   uint32_t b[MN2::L];
-  // A = a R, squared d1 times, parked in `row`
-  M.load_words(b, a + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{n2dev<MN2>(key).R2});
-  for (int k = 0; k < dmax; ++k) {
-    if (k < d1) {
-      M.store_strided(b, sq, st);
-      wave_sync_mem_();
-      M.mul(b, AStrided{sq, st});
-    }
-  }
+  // y as plain limbs, parked in `row` (c < n^2, so no reduction is needed)
+  M.load_words(b, yw, key.n2w);
   M.store_strided(b, row, st);
-  M.load_words(b, bw + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{n2dev<MN2>(key).R2});
+  M.load_words(b, xw, key.n2w);
+  M.mul(b, ARow{n2dev<MN2>(key).R2});  // x R
   for (int k = 0; k < dmax; ++k) {
-    if (k < d2) {
+    if (k < dx) {
       M.store_strided(b, sq, st);
       wave_sync_mem_();
       M.mul(b, AStrided{sq, st});
     }
   }
   wave_sync_mem_();
-  M.mul(b, AStrided{row, st});  // A B R
-  M.mul(b, AOne{});
+  M.mul(b, AStrided{row, st});  // x^(2^d) R * y * R^-1
   M.reduce_once(b);
   store_packed(M, b, row, st, out + (size_t)e * key.n2w, key.n2w);
   if (eout && MN2::G::g() == 0) eout[e] = emin;
@@ -1658,7 +1845,7 @@ __global__ void k_gap_pick(KeyDev key, const uint32_t* __restrict__ a, const int
                            uint32_t* __restrict__ x, uint32_t* __restrict__ k) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= count) return;
-  const int64_t d = (int64_t)ea[e] - (int64_t)eb[e];
+  const int64_t d = (int64_t)(ea ? ea[e] : 0) - (int64_t)(eb ? eb[e] : 0);  // NULL: all exponents 0
   const bool big = (d < 0 ? -d : d) >= dneg;
   const uint32_t* src = d > 0 ? a + (size_t)e * key.n2w : b + (size_t)e * key.n2w;
   uint32_t* xo = x + (size_t)e * key.n2w;
@@ -1726,6 +1913,49 @@ __global__ void __launch_bounds__(256, 2) k_djn_pub(KeyDev key, const uint32_t* 
   M.reduce_once(b);
   store_packed(M, b, ws + e, (int)count, out + (size_t)e * key.n2w, key.n2w);
 }
+
+#if XHE_NDIG
+// Public-key DJN encryption in Montgomery digits of n (2048 bits; the tables
+// rewritten as canonical digit pairs by k_tab_to_pmdx at key creation): the
+// first window's row is the start state, every further row is unpacked into
+// the group's LDS pairs and multiplied in (5 K^2 mads per product instead of
+// 2 S^2 on the 152-limb n^2); k_ndig_out folds in (1 + n m). Digit state out:
+// st [pair][count].
+template <class D, int RW>
+__global__ void __launch_bounds__(128, 2) k_djn_pub_nd(KeyDev key, const uint32_t* __restrict__ a_words, int aw,
+                                                       int64_t count, uint2* __restrict__ st) {
+  constexpr int GPB = 128 / D::TPI, L = D::L;
+  __shared__ uint2 ops_all[D::K * GPB];
+  __shared__ __attribute__((aligned(16))) uint32_t topc[D::K];
+  for (int i = threadIdx.x; i < D::K; i += blockDim.x) topc[i] = key.nd_topc[i];
+  __syncthreads();
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / D::TPI;
+  if (e >= count) return;
+  const int g = D::G::g();
+  uint2* ops = ops_all + threadIdx.x / D::TPI;
+  const uint32_t* tab = key.tab_n2;
+  const uint32_t* ae = a_words + (size_t)e * aw;
+  D X;
+  X.init(key.nd.N, key.nd.n0inv);
+  uint32_t a[L], c[L];
+  {
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, 0, row0);
+    const uint32_t* row = tab + (size_t)(row0 + d) * RW;
+    pmdx_load<D, 0>(a, row, RW / 2, g);
+    pmdx_load<D, 0>(c, row + RW / 2, RW / 2, g);
+  }
+  for (int w = 1; w < key.nwin; ++w) {
+    int64_t row0;
+    const uint32_t d = win_digit(key, ae, aw, w, row0);
+    pmdx_stage_row<D>(pmdx_launder(tab) + (size_t)(row0 + d) * RW, RW / 2, ops, GPB);
+    wave_sync_mem_();
+    X.template run<false>(a, c, OpLds{ops, GPB}, topc);
+    wave_sync_mem_();
+  }
+  ndig_st_store<D>(a, c, st, count, e);
+}
+#endif
 
 // Non-DJN obfuscation, variable base r with a uniform exponent:
 //   public  (paillier.py:228-230): (1 + n m) r^n mod n^2          -> out words
@@ -1950,7 +2180,9 @@ __global__ void __launch_bounds__(256, 2) k_nodjn_crt(KeyDev key, const uint32_t
 }
 
 // ---- homomorphic sums / histograms (A.9, decision_tree_trainer.py:151-160)
-// Each element enters as c^(2^d) R (Montgomery), d = e - e_min of its segment.
+// Each element enters as the plain residue c^(2^d), d = e - e_min of its
+// segment (no product when d = 0); the first level of k_chunk_prod chains the
+// plain residues and returns each chunk to Montgomery form with one product.
 template <class MN2>
 __global__ void __launch_bounds__(256, 2) k_align_mont(KeyDev key, const uint32_t* __restrict__ Nn2,
                                                        const uint32_t* __restrict__ c, const int32_t* __restrict__ d,
@@ -1963,26 +2195,32 @@ __global__ void __launch_bounds__(256, 2) k_align_mont(KeyDev key, const uint32_
   M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
   M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
-  M.mul(b, ARow{n2dev<MN2>(key).R2});
-  const int de = d ? d[e] : 0;
-  for (int k = 0; k < dmax; ++k) {
-    if (k < de) {
-      M.store_strided(b, sqws + e, st);
-      wave_sync_mem_();
-      M.mul(b, AStrided{sqws + e, st});
+  const int de = (d && dmax) ? d[e] : 0;
+  if (de > 0) {  // c^(2^d): into Montgomery form, d squarings, and out again
+    M.mul(b, ARow{n2dev<MN2>(key).R2});
+    for (int k = 0; k < dmax; ++k) {
+      if (k < de) {
+        M.store_strided(b, sqws + e, st);
+        wave_sync_mem_();
+        M.mul(b, AStrided{sqws + e, st});
+      }
     }
+    M.mul(b, AOne{});
+    M.reduce_once(b);
   }
-  M.reduce_once(b);
   M.store_strided(b, rows + e, st);
 }
 
-// One reduction level: chunk j multiplies rows [cbeg[j], cbeg[j+1]) (Montgomery
-// rows [S4][n_in]) into out row j ([S4][n_out]).
+// One reduction level: chunk j multiplies rows [cbeg[j], cbeg[j+1]) (rows
+// [S4][n_in]) into the Montgomery row j of out ([S4][n_out]). raw: the input
+// rows are plain residues and chunks are at most kRawChunk long: L plain
+// residues chain to P R^-(L-1), and one product by R^(L+1) gives P R - one
+// product per element plus one per chunk instead of two per element.
 template <class MN2>
 __global__ void __launch_bounds__(256, 2) k_chunk_prod(KeyDev key, const uint32_t* __restrict__ Nn2,
                                                        const uint32_t* __restrict__ in, int64_t n_in,
                                                        const int64_t* __restrict__ cbeg, int64_t n_out,
-                                                       uint32_t* __restrict__ outp) {
+                                                       uint32_t* __restrict__ outp, int raw) {
   const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (j >= n_out) return;
   MN2 M;
@@ -1995,6 +2233,7 @@ __global__ void __launch_bounds__(256, 2) k_chunk_prod(KeyDev key, const uint32_
   } else {
     M.load_strided(b, in + lo, (int)n_in);
     for (int64_t i = lo + 1; i < hi; ++i) M.mul(b, AStrided{in + i, (int)n_in});
+    if (raw) M.mul(b, ARow{n2dev<MN2>(key).Rpow + (size_t)(hi - lo + 1) * MN2::S4});
     M.reduce_once(b);
   }
   M.store_strided(b, outp + j, (int)n_out);

@@ -226,9 +226,12 @@ class PaillierContext(object):
         """Called by the batched encryptions: the policy's element counter."""
         self._volume = getattr(self, "_volume", 0) + int(count)
 
-    def device_key(self, device: int = 0):
-        """Device-resident key for this context on `device` (built once, cached;
-        rebuilt with wider tables when the window policy asks for them)."""
+    def device_key(self, device=None):
+        """Device-resident key for this context on `device` (default: the
+        process's own GPU, own_device(); built once, cached; rebuilt with
+        wider tables when the window policy asks for them)."""
+        if device is None:
+            device = self.own_device()
         dev = getattr(self, "_dev", None)
         if dev is None:
             dev = self._dev = {}

@@ -304,10 +304,20 @@ def fold_gap_powers(ctx, exps, seg_begin):
             elif m - ev[k] >= dneg:
                 drops.append((k, m - ev[k]))
             m = min(m, ev[k])
-        for i in range(len(ev)):
-            bigs = ([own[i]] if i in own else []) + [d for k, d in drops if k > i]
-            if bigs:
-                out[lo + i] = gap_power(ctx, ev[i] - m, bigs)
+        # one reverse pass: the drops at steps k > i as a running (count, shift
+        # sum, product of (2^s - n)), i.e. gap_power's factors without
+        # rebuilding the list per leaf
+        n = int(ctx.n)
+        dk = {k: d for k, d in drops}
+        cnt, ssum, prod = 0, 0, 1
+        for i in range(len(ev) - 1, -1, -1):
+            if i + 1 in dk:
+                d = dk[i + 1]
+                cnt, ssum, prod = cnt + 1, ssum + d, prod * ((1 << d) - n)
+            if i in own or cnt:
+                o = own.get(i)
+                ps, pp = (ssum + o, prod * ((1 << o) - n)) if o is not None else (ssum, prod)
+                out[lo + i] = (1 << (ev[i] - m - ps)) * pp
     return out
 
 
@@ -382,7 +392,7 @@ def segprod_words(ctx, cw, d, seg):
     src = cw if n else np.zeros((1, n2w), dtype=np.uint32)
     d = _i32(d)
     out = np.empty((nseg, n2w), dtype=np.uint32)
-    dk = ctx.device_key()
+    dk = ctx.device_key(ctx.own_device())  # the process's GPU, as _run and the resident path use
     nat.check(nat.lib().xhe_segprod_host(dk.handle, _vp(src), _vp(d) if dmax else None, dmax, n, _vp(seg), nseg,
                                          _vp(out)), "segprod")
     return out
@@ -399,7 +409,7 @@ def multiexp_words(ctx, bw, idx, kw_, kbits, win_bits=0):
     if ncols == 0 or nterms == 0 or bw.shape[0] == 0:
         raise ValueError("multiexp: empty problem")
     out = np.empty((ncols, n2w_of(ctx)), dtype=np.uint32)
-    dk = ctx.device_key()
+    dk = ctx.device_key(ctx.own_device())
     nat.check(nat.lib().xhe_multiexp_host(dk.handle, _vp(bw), bw.shape[0], _vp(iw), _vp(kw_), kw_.shape[1],
                                           int(kbits), ncols, nterms, int(win_bits), _vp(out)), "multiexp")
     return out

@@ -277,7 +277,8 @@ class Paillier(object):
             shape = data.shape
             flat = data.reshape(-1)
             n = flat.shape[0]
-            dev = resident.device_for(context, num_cores) if n else None
+            # ciphertext words + exponent + the staged plaintext per element
+            dev = resident.device_for(context, num_cores, n, 4 * ops.n2w_of(context) + 16) if n else None
             if flat.dtype.kind == "f":
                 if dev is not None:  # results stay in HBM (resident.py)
                     if obfuscation:

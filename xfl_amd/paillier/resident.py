@@ -47,13 +47,45 @@ def available():
     return _cuda_ok
 
 
-def device_for(ctx, num_cores=-1):
+# Share of the device's spare HBM (free + torch's cached blocks, less the
+# context's WIN_MARGIN table headroom) one new resident result may take;
+# larger batches stream through the host pipeline instead (xhe_*_host).
+RESIDENT_SHARE = 0.5
+
+
+def resident_budget(ctx, dev):
+    """Bytes a new resident batch may occupy on `dev` ($XHE_RESIDENT_MAX_BYTES
+    overrides; None = unknown, no cap)."""
+    pin = os.environ.get("XHE_RESIDENT_MAX_BYTES", "").strip()
+    if pin:
+        return int(pin)
+    from .._native import device_free_bytes
+    free = device_free_bytes(dev)
+    if free is None:
+        return None
+    torch = _torch()
+    try:
+        free += int(torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
+    except Exception:  # noqa: BLE001
+        pass
+    return int(max(0, free - getattr(ctx, "WIN_MARGIN", 0)) * RESIDENT_SHARE)
+
+
+def device_for(ctx, num_cores=-1, count=0, elem_bytes=0):
     """The GPU whose HBM holds this context's arrays, or None (host-buffer
-    mode: sharded contexts, $XHE_RESIDENT=0, no GPU)."""
+    mode: sharded contexts, $XHE_RESIDENT=0, no GPU, or a new batch of
+    `count` results of `elem_bytes` each - ciphertext words, exponent and
+    the plaintext staged for it - above resident_budget())."""
     if ctx is None or os.environ.get("XHE_RESIDENT", "1").strip() == "0" or not available():
         return None
     devs = ctx.shard_devices(num_cores)
-    return devs[0] if len(devs) == 1 else None
+    if len(devs) != 1:
+        return None
+    if count and elem_bytes:
+        cap = resident_budget(ctx, devs[0])
+        if cap is not None and count * elem_bytes > cap:
+            return None
+    return devs[0]
 
 
 def stream(dev):

@@ -100,16 +100,21 @@ class GatherPipeline:
     produce(i, buf) writes step i's shard ([rows, words] int32) into buf.
     With world > 1 the shard and the gathered vector are double-buffered and
     the gather is issued async_op, so step i's all-gather (RCCL's stream)
-    overlaps step i+1's kernels; drain() waits for every pending gather."""
+    overlaps step i+1's kernels; drain() waits for every pending gather.
+    collective=True takes the gather path at world 1 too (an initialised
+    process group of one rank: bench.py --dist, tests/test_gpu_rccl.py), so
+    the RCCL calls of the N-GPU job run on a one-GPU box; the default is
+    world > 1."""
 
-    def __init__(self, produce, rows, words, world=1, rank=0, device="cpu", group=None, depth=2):
+    def __init__(self, produce, rows, words, world=1, rank=0, device="cpu", group=None, depth=2, collective=None):
         self.produce = produce
         self.world, self.rank, self.group = world, rank, group
         self.rows = rows
-        self.nb = depth if world > 1 else 1
+        self.coll = world > 1 if collective is None else bool(collective)
+        self.nb = depth if self.coll else 1
         self.shards = [torch.empty((rows, words), dtype=torch.int32, device=device) for _ in range(self.nb)]
         self.gathered = ([torch.empty((world * rows, words), dtype=torch.int32, device=device) for _ in range(self.nb)]
-                         if world > 1 else None)
+                         if self.coll else None)
         self.pending = [None] * self.nb
 
     def step(self, i):
@@ -119,7 +124,7 @@ class GatherPipeline:
             self.pending[b] = None
         buf = self.shards[b]
         self.produce(i, buf)
-        if self.world > 1:
+        if self.coll:
             self.pending[b] = dist.all_gather_into_tensor(self.gathered[b], buf, group=self.group, async_op=True)
         return buf
 
@@ -130,9 +135,9 @@ class GatherPipeline:
                 self.pending[b] = None
 
     def vector(self, i):
-        """The reassembled vector of step i (after drain); the shard itself when world == 1."""
+        """The reassembled vector of step i (after drain); the shard itself without a collective."""
         b = i % self.nb
-        return self.gathered[b] if self.world > 1 else self.shards[b]
+        return self.gathered[b] if self.coll else self.shards[b]
 
     def shard(self, i):
         return self.shards[i % self.nb]
@@ -152,7 +157,7 @@ def shard_parity(shard, vector, rank, idx, expected):
 
 
 # ------------------------------------------------------------ partial merge
-def merge_segment_products(partials, exps, combine, counts=None, group=None):
+def merge_segment_products(partials, exps, combine, counts=None, group=None, collective=None):
     """Merge every rank's per-segment homomorphic sums (histogram bins).
 
     partials [nseg, words] int32 and exps [nseg] int32: this rank's segment
@@ -167,7 +172,8 @@ def merge_segment_products(partials, exps, combine, counts=None, group=None):
     groupby 'count' column). Returns (words, exponents, counts)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     nseg, words = partials.shape
-    if world > 1:
+    coll = world > 1 if collective is None else (bool(collective) and dist.is_initialized())
+    if coll:
         dev = partials.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
         allp = torch.empty((world * nseg, words), dtype=torch.int32, device=dev)
         dist.all_gather_into_tensor(allp, partials.to(dev).contiguous(), group=group)
