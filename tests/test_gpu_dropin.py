@@ -63,6 +63,18 @@ def test_mulmod_gap_c_abi():
     torch.cuda.synchronize()
     assert nat.words_to_ints(out.cpu().numpy().view(np.uint32)) == [hx(r) for r in ops["gap_add_pub"]["raw"]]
     assert eo.tolist() == ops["gap_add_pub"]["exp"]
+    # one exponent array NULL (= all 0, include/xhe.h): the same gaps relative
+    # to it take the same negative branch (the fix runs whenever dmax >= dneg)
+    want = [hx(r) for r in ops["gap_add_pub"]["raw"]]
+    for null_a in (True, False):
+        rel = (eb - ea) if null_a else (ea - eb)
+        nat.check(nat.lib().xhe_mulmod(dk.handle, a.data_ptr(), None if null_a else rel.data_ptr(), b.data_ptr(),
+                                       rel.data_ptr() if null_a else None, len(pairs), dmax, out.data_ptr(),
+                                       eo.data_ptr(), s), "mulmod")
+        torch.cuda.synchronize()
+        assert nat.words_to_ints(out.cpu().numpy().view(np.uint32)) == want, null_a
+        shift = ea if null_a else eb
+        assert eo.tolist() == [e - int(d) for e, d in zip(ops["gap_add_pub"]["exp"], shift.tolist())]
 
 
 @pytest.mark.parametrize("fx", FIXTURES)

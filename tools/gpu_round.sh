@@ -34,6 +34,22 @@ for s in $STEPS; do
       timeout -k 10 600 python -u tools/lr_he_demo.py --epochs 3 --check > "$OUT/lr_demo.json" 2> "$OUT/lr_demo.err" || { tail -20 "$OUT/lr_demo.err"; exit 3; }
       tail -c 1500 "$OUT/lr_demo.json"
       ;;
+    lrtrace)
+      # rocprofv3 kernel trace of the LR demo (config 1): per-kernel split of a batch
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/lr_trace" -o lr --output-format csv -- \
+        python3 -u tools/lr_he_demo.py --epochs 3 --check > "$OUT/lr_demo_prof.json" 2> "$OUT/lr_trace.err" \
+        || { tail -20 "$OUT/lr_trace.err"; exit 3; }
+      tail -c 600 "$OUT/lr_demo_prof.json"
+      ;;
+    opstrace)
+      # kernel trace of the bench incl. the secondary operations (ops)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/ops_trace" -o ops --output-format csv -- \
+        python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_ops_prof.json" 2> "$OUT/ops_trace.err" \
+        || { tail -20 "$OUT/ops_trace.err"; exit 3; }
+      ;;
+    configs)
+      bash tools/gpu_configs.sh "$TAG/configs" || exit $?
+      ;;
     *)
       echo "unknown step $s"; exit 2
       ;;

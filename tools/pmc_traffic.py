@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -21,10 +22,13 @@ def per_dispatch(d, kernel):
     out = collections.defaultdict(lambda: collections.defaultdict(float))
     grid = {}
     for r in rows:
-        if kernel not in r["Kernel_Name"]:
+        m = re.search(r"(\w+)\s*(?:<|\()", r["Kernel_Name"])  # the kernel's own name (k_djn_pmd, not k_djn_pmdx)
+        if not m or m.group(1) != kernel:
             continue
         out[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
+        if "Start_Timestamp" in r:
+            out[r["Dispatch_Id"]]["_duration_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     return out, grid
 
 
@@ -58,6 +62,18 @@ def main():
                     "correction": "fetch = 2 x FETCH_SIZE KiB (gfx950 16-B/lane reads), write = WRITE_SIZE KiB"})
     if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg:
         rec["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+    # clock from SQ_BUSY_CYCLES (32 SQs: 8 XCDs x 4 SEs), then the VALU issue
+    # fraction: a wave64 VALU instruction takes 4 cycles of its SIMD, 1024 SIMDs
+    dur = avg.get("_duration_ns")
+    if dur and "SQ_BUSY_CYCLES" in avg:
+        clk = avg["SQ_BUSY_CYCLES"] / (dur * 1e-9) / 32
+        rec["duration_ms"] = dur * 1e-6
+        rec["clock_ghz"] = clk / 1e9
+        quad_cycles = dur * 1e-9 * clk / 4 * 1024
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            rec["valu_busy_frac"] = avg["SQ_ACTIVE_INST_VALU"] / quad_cycles
+    if dur and "SQ_INSTS_VALU" in avg and rec.get("clock_ghz"):
+        rec["valu_issue_frac"] = avg["SQ_INSTS_VALU"] / (dur * 1e-9 * rec["clock_ghz"] * 1e9 / 4 * 1024)
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     with open(dst, "w") as f:
         json.dump(rec, f, indent=1)

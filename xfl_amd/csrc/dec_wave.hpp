@@ -33,6 +33,14 @@
 
 namespace xhe {
 
+#ifndef XHE_WAVE_FUSED
+// 1: the normalisations fused into the next product's operand reads (4 LDS
+// phases per product instead of 6). Measured slower (k_dec_wave 2.23 -> 3.22
+// ms for 15 elements under rocprof): every thread of a slice recomputes the
+// slice's 16 limbs from 3 x 18 column reads (37x redundant LDS traffic), more
+// than the sync it saves. Kept as an A/B switch.
+#define XHE_WAVE_FUSED 0
+#endif
 #ifndef XHE_WAVE_PROF
 #define XHE_WAVE_PROF 0  // dev builds: cycles per phase of block (0, 0), printed at the end
 #endif
@@ -63,12 +71,14 @@ __device__ unsigned long long g_wave_t;
 // and the quads past the triangle of nonzero terms (z is zero there): 2.2x
 // the mads of the exact column sums, cheap next to the LDS round trips that
 // set a product's latency.
-template <int K, int NWV>
+template <int K, int NWV, int W_ = 28>
 struct WaveMont {
-  static constexpr int W = 28;
+  static constexpr int W = W_;  // 28 mod P^2 (k_dec_wave); 27 mod n^2 (k_mexp_horner_wave: 2K W-bit
+                                // products per column stay below 2^64 at K = 154)
   static constexpr uint32_t MASK = (1u << W) - 1u;
   static constexpr int NT = 64 * NWV;  // threads per residue
-  static constexpr int TS = NWV >= 8 ? 8 : 16;  // terms per slice
+  // terms per slice: 8 when the threads hold every (quad, 8-term slice), else 16
+  static constexpr int TS = ((2 * K - 1 + 3) / 4) * ((K + 7) / 8) <= NT ? 8 : 16;
   static constexpr int NS = (K + TS - 1) / TS;
   static constexpr int NQF = (2 * K - 1 + 3) / 4, NQL = (K + 3) / 4;
   static_assert(NQF * NS <= NT, "one (quad, slice) per thread");
@@ -121,15 +131,35 @@ struct WaveMont {
   // (consecutive term quads share one), 4 TS mads into four accumulators
   // (one per column), then one LDS atomic per column. LO: columns < K + 2
   // only (the quotient product; its columns from K on are never read).
-  template <bool LO>
-  static XHE_DEV void prodq(const uint32_t* a, const uint32_t* z, uint64_t* col) {
+  // FUSED: the multiplier is norm() of the lazy columns acg (= col + G)
+  // below limb K, formed by each thread for its own slice of terms straight
+  // from the columns (no normalisation phase and no sync before the
+  // product); else the limbs a. ZERO: the idle threads zero the other
+  // column buffer (last read by the previous product's tail, next written
+  // by the next product).
+  template <bool LO, bool FUSED = false>
+  static XHE_DEV void prodq(const uint32_t* a, const uint64_t* acg, const uint32_t* z, uint64_t* col,
+                            uint64_t* zero = nullptr) {
     constexpr int NQ = LO ? NQL : NQF;
     const int q = tid() % NQ, sl = tid() / NQ;
     if (sl < NS) {
       const int t0 = sl * TS;
       uint4 av[TS / 4], zq[TS / 4 + 1];
+      if constexpr (FUSED) {
+        // split3 of columns t0-1 .. t0+TS-1 (reads columns t0-3 .. t0+TS-1;
+        // the G guards below column 0 are zero), then the second pass
+        uint32_t s3[TS + 1];
 #pragma unroll
-      for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
+        for (int k = 0; k <= TS; ++k) s3[k] = t0 - 1 + k < K ? split3(acg, t0 - 1 + k) : 0u;  // (mcol ends at 4 NQL)
+        uint32_t v[TS];
+#pragma unroll
+        for (int k = 0; k < TS; ++k) v[k] = t0 + k < K ? (s3[k + 1] & MASK) + (s3[k] >> W) : 0u;
+#pragma unroll
+        for (int u = 0; u < TS / 4; ++u) av[u] = make_uint4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
+      }
       // quad u of terms needs Z[B_u - 4 .. B_u + 3], B_u = ZO + 4q - t0 - 4u:
       // zq[u + 1] = Z[B_u - 4 ..], zq[u] = Z[B_u ..]
       const uint32_t* zb0 = z + (ZO + 4 * q - t0);
@@ -147,6 +177,8 @@ struct WaveMont {
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long*)&col[G + 4 * q + i], (unsigned long long)acc[i]);
+    } else if (zero) {
+      for (int i = tid() - NQ * NS; i < 2 * K; i += NT - NQ * NS) zero[G + i] = 0ull;
     }
     sync();
   }
@@ -156,6 +188,8 @@ struct WaveMont {
   // v_(K-1) >= MASK - 1 (the limbs below sum to < 2^(W (K-1)) (1 + 3/MASK)),
   // else every v_j is 0: the carry out of the low part is v_(K-1) != 0, which
   // every thread reads for itself (no ballot).
+  // (the threads from K on zero mcol: last read by this product's U phase,
+  // next written by the next product's quotient)
   static XHE_DEV void tail(Lds& s, int cur, uint32_t* dst, bool zbw) {
     const uint64_t* cg = s.col[cur] + G;
     const uint32_t k = norm(cg, K - 1) != 0u ? 1u : 0u;
@@ -167,6 +201,7 @@ struct WaveMont {
       dst[i] = v;
       if (zbw) s.zb[ZO + i] = v;
     }
+    for (int i = tid() - K; i >= 0 && i < 4 * NQL; i += NT - K) s.mcol[G + i] = 0ull;
     sync();
   }
 
@@ -190,14 +225,24 @@ struct WaveMont {
     sync();
   }
 
-  // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N)
+  // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N). Three
+  // phases: the quotient product reads T mod R straight from the columns,
+  // the U product reads m from its columns (round 4; the separate
+  // normalisation phases before each took 6 phases per product to 4).
   static XHE_DEV void reduce(Lds& s, int cur, uint32_t* dst, bool zbw) {
+#if XHE_WAVE_FUSED
+    prodq<true, true>(nullptr, s.col[cur] + G, s.znp, s.mcol, s.col[cur ^ 1]);  // m = (T mod R) N' mod R
+    XHE_WAVE_T(1);
+    prodq<false, true>(nullptr, s.mcol + G, s.zn, s.col[cur]);  // U = T + m N
+    XHE_WAVE_T(2);
+#else
     norm_low_t(s, cur);
-    prodq<true>(s.tl, s.znp, s.mcol);  // m = (T mod R) N' mod R
+    prodq<true>(s.tl, nullptr, s.znp, s.mcol);  // m = (T mod R) N' mod R
     XHE_WAVE_T(1);
     norm_low(s.mcol, s.mq);
-    prodq<false>(s.mq, s.zn, s.col[cur]);  // U = T + m N
+    prodq<false>(s.mq, nullptr, s.zn, s.col[cur]);  // U = T + m N
     XHE_WAVE_T(2);
+#endif
     tail(s, cur, dst, zbw);
     XHE_WAVE_T(3);
   }
@@ -207,7 +252,7 @@ struct WaveMont {
   static XHE_DEV void mul(Lds& s, int& cur, const uint32_t* a, uint32_t* dst, bool zbw) {
     cur ^= 1;
     XHE_WAVE_T(-1);
-    prodq<false>(a, s.zb, s.col[cur]);
+    prodq<false>(a, nullptr, s.zb, s.col[cur]);
     XHE_WAVE_T(0);
     reduce(s, cur, dst, zbw);
   }
@@ -372,6 +417,186 @@ __global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_
       printf("wave prof (cycles, all products): prod1 %llu prod2 %llu prod3 %llu tail %llu total %llu\n",
              g_wave_prof[0], g_wave_prof[1] - 0, g_wave_prof[2], g_wave_prof[3], clock64() - g_wave_prof[7]);
 #endif
+  }
+}
+
+}  // namespace xhe
+
+namespace xhe {
+
+// ---------------------------------------------------------------------------
+// Horner of the encrypted mat-vec (k_mexp_horner) with one block of NWV waves
+// per column, for the small batches of the LR step (2048-bit keys; the
+// 16-lane shape's P rows). out[j] = prod_w P[j][w]^(2^(c w)) is a chain of
+// ~kbits squarings and nwin - 1 products - latency, ~10 us per product in the
+// 16-lane shape - so here each product is WaveMont's column product (4 LDS
+// phases, no serial digit chain) mod n^2 in 154 limbs of 27 bits (R_w =
+// 2^4158). The P rows are Montgomery rows of the 16-lane shape (P R_X, R_X =
+// 2^(27*160), limbs of the same 27 bits, canonical so limbs from 154 on are
+// zero): MontW(P R_X, C) with C = R_w^2 R_X^-1 mod n^2 puts P into wave form,
+// and a window product is MontW(MontW(acc, P R_X), C) = acc P (wave form).
+// Out: MontW(1, acc) = the plain product (< 2N), normalised, reduced once and
+// packed to n2w words by one thread.
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_mexp_horner_wave(KeyDev key, const uint32_t* __restrict__ P, int nwin,
+                                                               int c, int64_t ncols, uint32_t* __restrict__ out) {
+  using WM = WaveMont<K, NWV, 27>;
+  constexpr uint32_t MASK = WM::MASK;
+  constexpr int NT = WM::NT;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int l = WM::tid();
+  const int64_t j = blockIdx.x;
+  {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+    for (int i = l; i < (int)(sizeof(s) / 4); i += NT) w[i] = 0u;
+  }
+  WM::sync();
+  for (int i = l; i < K; i += NT) {
+    s.zn[WM::ZO + i] = key.n2w_N[i];
+    s.znp[WM::ZO + i] = key.n2w_np[i];
+    s.r3[i] = key.n2w_C[i];  // C = R_w^2 R_X^-1 (the a-operand of the second window product)
+    s.zb[WM::ZO + i] = key.n2w_C[i];
+  }
+  if (l == 0) s.one[0] = 1u;
+  const int64_t pst = ncols * nwin;  // P: [limb][ncols * nwin], column j's window w at j * nwin + w
+  auto load_p = [&](int w) {
+    const uint32_t* pj = P + j * nwin + w;
+    for (int i = l; i < K; i += NT) s.tl[i] = pj[(size_t)i * pst];
+  };
+  load_p(nwin - 1);
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, true);  // P_top R_X C / R_w = P_top R_w
+  for (int w = nwin - 2; w >= 0; --w) {
+#pragma unroll 1
+    for (int r = 0; r < c; ++r) WM::mul(s, cur, s.x, s.x, true);  // acc^2 (a = zb = acc)
+    load_p(w);
+    WM::sync();
+    WM::mul(s, cur, s.tl, s.x, true);  // acc P R_X / R_w
+    WM::mul(s, cur, s.r3, s.x, true);  // * C / R_w: acc P (wave form)
+  }
+  WM::mul(s, cur, s.one, s.x, false);  // plain, < 2N, limbs <= MASK + 2
+  if (l == 0) {
+    // normalise, subtract N once if x >= N, pack to n2w words
+    uint32_t cy = 0;
+    for (int i = 0; i < K; ++i) {
+      const uint32_t t = s.x[i] + cy;
+      s.x[i] = t & MASK;
+      cy = t >> WM::W;
+    }
+    int64_t br = 0;
+    for (int i = 0; i < K; ++i) br = ((int64_t)s.x[i] - (int64_t)s.zn[WM::ZO + i] + br) >> WM::W;
+    if (br == 0) {  // x >= N
+      br = 0;
+      for (int i = 0; i < K; ++i) {
+        const int64_t t = (int64_t)s.x[i] - (int64_t)s.zn[WM::ZO + i] + br;
+        s.x[i] = (uint32_t)t & MASK;
+        br = t >> WM::W;
+      }
+    }
+    uint32_t* o = out + (size_t)j * key.n2w;
+    uint64_t acc = 0;
+    int have = 0, wi = 0;
+    for (int i = 0; i < K && wi < key.n2w; ++i) {
+      acc |= (uint64_t)s.x[i] << have;
+      have += WM::W;
+      while (have >= 32 && wi < key.n2w) {
+        o[wi++] = (uint32_t)acc;
+        acc >>= 32;
+        have -= 32;
+      }
+    }
+    while (wi < key.n2w) {
+      o[wi++] = (uint32_t)acc;
+      acc >>= 32;
+    }
+  }
+}
+
+
+// Ciphertext add with exponent alignment for small batches (2048-bit keys; the
+// LR step's "+ noise", paillier.py:106-123, 79-86): out = x^(2^d) y mod n^2
+// with x the operand of larger exponent, d its gap - a chain of d squarings
+// (~10 us each in the 16-lane shape) - here one block of NWV waves per
+// element: x R_w = MontW(x, R_w^2 mod n^2), d squarings, MontW(x^(2^d) R_w,
+// y) = x^(2^d) y (plain), normalised and packed by one thread. eout = the
+// smaller exponent (as k_mulmod_n2).
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_mulmod_wave(KeyDev key, const uint32_t* __restrict__ a,
+                                                          const int32_t* __restrict__ ea, const uint32_t* __restrict__ b,
+                                                          const int32_t* __restrict__ eb, int64_t count,
+                                                          uint32_t* __restrict__ out, int32_t* __restrict__ eout) {
+  using WM = WaveMont<K, NWV, 27>;
+  constexpr uint32_t MASK = WM::MASK;
+  constexpr int NT = WM::NT;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int l = WM::tid();
+  const int64_t e = blockIdx.x;
+  {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+    for (int i = l; i < (int)(sizeof(s) / 4); i += NT) w[i] = 0u;
+  }
+  WM::sync();
+  const int e1 = ea ? ea[e] : 0, e2 = eb ? eb[e] : 0;
+  const bool xb = e2 > e1;
+  const int d = (xb ? e2 - e1 : e1 - e2);
+  const uint32_t* xw = (xb ? b : a) + (size_t)e * key.n2w;
+  const uint32_t* yw = (xb ? a : b) + (size_t)e * key.n2w;
+  // W-bit limbs of x into tl (a-operand), y into r3, R_w^2 into the multiplicand
+  auto limbs = [&](const uint32_t* wv, uint32_t* dst) {
+    for (int i = l; i < K; i += NT) {
+      const int bit = WM::W * i, k = bit >> 5, sh = bit & 31;
+      const uint32_t lo = k < key.n2w ? wv[k] : 0u, hi = k + 1 < key.n2w ? wv[k + 1] : 0u;
+      dst[i] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
+    }
+  };
+  limbs(xw, s.tl);
+  limbs(yw, s.r3);
+  for (int i = l; i < K; i += NT) {
+    s.zn[WM::ZO + i] = key.n2w_N[i];
+    s.znp[WM::ZO + i] = key.n2w_np[i];
+    s.zb[WM::ZO + i] = key.n2w_R2[i];
+  }
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, true);  // x R_w
+#pragma unroll 1
+  for (int r = 0; r < d; ++r) WM::mul(s, cur, s.x, s.x, true);  // squarings (a = zb = x)
+  WM::mul(s, cur, s.r3, s.x, false);  // y x^(2^d) R_w / R_w: plain, < 2N
+  if (l == 0) {
+    uint32_t cy = 0;
+    for (int i = 0; i < K; ++i) {
+      const uint32_t t = s.x[i] + cy;
+      s.x[i] = t & MASK;
+      cy = t >> WM::W;
+    }
+    int64_t br = 0;
+    for (int i = 0; i < K; ++i) br = ((int64_t)s.x[i] - (int64_t)s.zn[WM::ZO + i] + br) >> WM::W;
+    if (br == 0) {
+      br = 0;
+      for (int i = 0; i < K; ++i) {
+        const int64_t t = (int64_t)s.x[i] - (int64_t)s.zn[WM::ZO + i] + br;
+        s.x[i] = (uint32_t)t & MASK;
+        br = t >> WM::W;
+      }
+    }
+    uint32_t* o = out + (size_t)e * key.n2w;
+    uint64_t acc = 0;
+    int have = 0, wi = 0;
+    for (int i = 0; i < K && wi < key.n2w; ++i) {
+      acc |= (uint64_t)s.x[i] << have;
+      have += WM::W;
+      while (have >= 32 && wi < key.n2w) {
+        o[wi++] = (uint32_t)acc;
+        acc >>= 32;
+        have -= 32;
+      }
+    }
+    while (wi < key.n2w) {
+      o[wi++] = (uint32_t)acc;
+      acc >>= 32;
+    }
+    if (eout) eout[e] = e1 < e2 ? e1 : e2;
   }
 }
 

@@ -328,6 +328,16 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   size_t o_nlim = bl.put_limbs(n, k->mp2);
   ModOff o_n2m = put_mod(bl, n2, k->mn2, kRpowRows);
   ModOff o_n2X = put_mod(bl, n2, k->mn2X, kRpowRows);
+  size_t o_n2wN = 0, o_n2wnp = 0, o_n2wC = 0, o_n2wR2 = 0;
+  if (K == 2048) {  // k_mexp_horner_wave
+    const ModSpec sw{154, 27};
+    const BigU Rw = pow2((size_t)27 * 154), RX = pow2((size_t)k->mn2X.W * k->mn2X.S);
+    o_n2wN = bl.put_limbs(n2, sw);
+    o_n2wnp = bl.put_limbs(sub(Rw, modinv(n2, Rw)), sw);
+    const BigU Rwn = mod(Rw, n2);
+    o_n2wC = bl.put_limbs(mulmod(mulmod(Rwn, Rwn, n2), modinv(mod(RX, n2), n2), n2), sw);
+    o_n2wR2 = bl.put_limbs(mulmod(Rwn, Rwn, n2), sw);
+  }
   size_t o_nR2n2, o_hMn2 = 0;
   {
     BigU Rn2 = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
@@ -371,7 +381,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     // R^2 R_MN2^-1 (R_MN2 = 2^(27*152), the public DJN tables' Montgomery
     // factor): converts their rows to canonical digits (k_tab_to_pmdx, n)
     const BigU RM = mod(pow2((size_t)k->mn2.W * k->mn2.S), n2);
-    on.dwt = digits(mulmod(mulmod(R2, R2, n2), mulmod(R2, modinv(RM, n2), n2), n2));
+    on.dwt = digits(mulmod(mulmod(R2, R2, n2), modinv(RM, n2), n2));  // X = w R^2, w = R^2 R_MN2^-1
     std::vector<uint32_t> tc = submod(BigU(1), Rn, n).to_limbs(27, 80);
     for (auto& x : tc) x += (1u << 27) - 1u;
     on.topc = bl.put(tc);
@@ -560,6 +570,12 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   kd.n_lim = B + o_nlim;
   kd.n2 = moddev(B, o_n2m);
   kd.n2X = moddev(B, o_n2X);
+  if (K == 2048) {
+    kd.n2w_N = B + o_n2wN;
+    kd.n2w_np = B + o_n2wnp;
+    kd.n2w_C = B + o_n2wC;
+    kd.n2w_R2 = B + o_n2wR2;
+  }
   kd.nR2_n2 = B + o_nR2n2;
   kd.n_bits = (int)n.bits();
 #if XHE_NDIG
@@ -1082,8 +1098,7 @@ void encrypt_nodjn_pmd(const xhe_key* k, const uint32_t* m, const uint32_t* r, i
     {
       ProfScope ps("k_nodjn_crt", s);
       hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3((unsigned)std::min<int64_t>((n + 127) / 128, pow_blocks), 2),
-                         dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.ep_words, k->kd.ep_bits, k->kd.eq_words,
-                         k->kd.eq_bits, n, st, ws);
+                         dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, 1, n, st, ws);
       HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL((k_nodjn_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
@@ -1194,9 +1209,31 @@ bool n2_row(int64_t count) {
   return pin ? pin == 16 : count <= kN2RowMax;
 }
 
+// Aligned adds of a few elements with long alignment chains run one 16-wave
+// block per element (k_mulmod_wave, 2048-bit keys): up to kWaveAddMax
+// elements when the largest gap is at least kWaveAddMinD squarings.
+// $XHE_ADD_WAVE=0 keeps the lane shapes (A/B).
+constexpr int64_t kWaveAddMax = 256;
+constexpr int kWaveAddMinD = 4;
+bool add_wave_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_ADD_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class Sh, class MN2 = typename Sh::MN2>
 void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const uint32_t* b, const int32_t* eb,
                  int64_t count, int dmax, uint32_t* out, int32_t* eout, hipStream_t s) {
+  if constexpr (Sh::K == 2048) {
+    if (count <= kWaveAddMax && dmax >= kWaveAddMinD && add_wave_on()) {
+      hipLaunchKernelGGL((k_mulmod_wave<154, 16>), dim3((unsigned)count), dim3(1024), 0, s, k->kd, a, ea, b, eb, count,
+                         out, eout);
+      HIPCHK(hipGetLastError());
+      return;
+    }
+  }
   int64_t chunk = std::min<int64_t>(count, kChunk);
   uint32_t* ws = nullptr;
   ws_alloc((void**)&ws, (size_t)2 * MN2::S4 * chunk * sizeof(uint32_t), s);
@@ -1323,41 +1360,65 @@ template <class Sh, class MN2 = typename Sh::MN2>
 uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s,
                           bool raw = false) {
   const int S4 = MN2::S4;
-  const int64_t C = kRawChunk;  // chunk length per level
   const int64_t nseg = (int64_t)seg.size() - 1;
+  // Lane groups the chip holds at 2 waves per SIMD: while a level has at least
+  // that many chunks of kRawChunk rows it is throughput-bound and takes long
+  // chunks; above that the levels are latency-bound (a chunk is a chain of
+  // dependent products), and chunks of 4 give the shortest chain in all
+  // (log4 levels x 4 products, against log32 levels x 32).
+  constexpr int64_t kFill = 131072 / MN2::TPI;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
+  // plan every level on the host first: the chunk boundaries of all levels go
+  // up in one copy, and the levels run back to back without a host sync
+  struct Level {
+    size_t cb_off;
+    int64_t n_in, n_out;
+    bool raw;
+  };
+  std::vector<int64_t> all_cb;
+  std::vector<Level> plan;
   int64_t n_cur = count;
-  uint32_t* cur = rows;
+  bool first = true;
   while (true) {
-    bool done = true;
+    bool ones = true;  // every segment is one row: nothing left to multiply
     for (int64_t i = 0; i < nseg; ++i)
-      if (seg[i + 1] - seg[i] != 1) { done = false; break; }
-    // chunk boundaries: each segment split into ceil(len/C) chunks (>= 1 chunk)
-    std::vector<int64_t> cb{0}, nseg_b{0};
+      if (seg[i + 1] - seg[i] != 1) {
+        ones = false;
+        break;
+      }
+    if (ones && !(first && raw)) break;  // (plain rows still need Montgomery form)
+    const int64_t C = (first && raw) || n_cur / kRawChunk >= kFill ? kRawChunk : 4;
+    std::vector<int64_t> nseg_b{0};
+    const size_t off = all_cb.size();
+    all_cb.push_back(0);
     for (int64_t i = 0; i < nseg; ++i) {
-      int64_t len = seg[i + 1] - seg[i];
-      int64_t nch = done ? 1 : std::max<int64_t>(1, (len + C - 1) / C);
-      for (int64_t t = 0; t < nch; ++t) cb.push_back(std::min(seg[i + 1], seg[i] + (t + 1) * (done ? len : C)));
+      const int64_t len = seg[i + 1] - seg[i];
+      const int64_t nch = std::max<int64_t>(1, (len + C - 1) / C);  // an empty segment: one (empty) chunk
+      for (int64_t t = 0; t < nch; ++t) all_cb.push_back(std::min(seg[i + 1], seg[i] + (t + 1) * C));
       nseg_b.push_back(nseg_b.back() + nch);
     }
-    int64_t n_out = (int64_t)cb.size() - 1;
-    int64_t* dcb = nullptr;
-    uint32_t* nxt = nullptr;
-    HIPCHK(hipMallocAsync((void**)&dcb, cb.size() * 8, s));
-    HIPCHK(hipMemcpyAsync(dcb, cb.data(), cb.size() * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(n_out, 1) * 4, s));
-    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, n_cur, dcb, n_out,
-                       nxt, raw ? 1 : 0);
-    raw = false;  // every later level multiplies Montgomery rows
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));  // cb lives on the host stack
-    (void)hipFree(dcb);
-    (void)hipFree(cur);
-    cur = nxt;
+    const int64_t n_out = (int64_t)(all_cb.size() - off) - 1;
+    plan.push_back({off, n_cur, n_out, first && raw});
     n_cur = n_out;
-    seg = nseg_b;
-    if (done) break;
+    seg.swap(nseg_b);
+    first = false;
   }
+  if (plan.empty()) return rows;  // already one Montgomery row per segment
+  int64_t* dcb = nullptr;
+  HIPCHK(hipMallocAsync((void**)&dcb, all_cb.size() * 8, s));
+  HIPCHK(hipMemcpyAsync(dcb, all_cb.data(), all_cb.size() * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // all_cb is host memory of this frame (one sync per call)
+  uint32_t* cur = rows;
+  for (const Level& L : plan) {
+    uint32_t* nxt = nullptr;
+    HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(L.n_out, 1) * 4, s));
+    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(L.n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, L.n_in,
+                       dcb + L.cb_off, L.n_out, nxt, L.raw ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipFreeAsync(cur, s));
+    cur = nxt;
+  }
+  HIPCHK(hipFreeAsync(dcb, s));
   return cur;
 }
 
@@ -1381,8 +1442,8 @@ void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dma
   hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, nseg, out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
-  (void)hipFree(cur);
-  (void)hipFree(sq);
+  (void)hipFreeAsync(cur, s);
+  (void)hipFreeAsync(sq, s);
 }
 
 // Window bits for a multi-exponentiation: minimise table products
@@ -1414,8 +1475,14 @@ void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, cons
   HIPCHK(hipMallocAsync((void**)&tab, ((size_t)nbases << c) * S4 * 4, s));
   {
     ProfScope ps("k_mexp_tab", s);
-    hipLaunchKernelGGL(k_mexp_tab<MN2>, blocks(nbases), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, bases, nbases, c, tab);
-    HIPCHK(hipGetLastError());
+    // by levels of entries (c + 1 dependent products per base); one launch
+    // per level
+    for (int lvl = 1; lvl <= c; ++lvl) {
+      const int64_t per = lvl <= 1 ? 1 : lvl < c ? ((int64_t)1 << (lvl - 1)) : ((int64_t)1 << (lvl - 1)) - 1;
+      hipLaunchKernelGGL(k_mexp_tab_lvl<MN2>, blocks(nbases * per), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, bases,
+                         nbases, c, lvl, tab);
+      HIPCHK(hipGetLastError());
+    }
   }
   // enough lane groups to fill the chip, at least 2 terms per group
   const int64_t segs = ncols * nwin;
@@ -1434,13 +1501,30 @@ void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, cons
   for (int64_t i = 0; i <= segs; ++i) seg[i] = i * nchunks;
   uint32_t* P = reduce_segments<Sh, MN2>(k, rows, n_out, std::move(seg), s);
   HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * ncols * 4, s));
-  hipLaunchKernelGGL(k_mexp_horner<MN2>, blocks(ncols), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, P, nwin, c, ncols, sq,
-                     out);
-  HIPCHK(hipGetLastError());
+  {
+    ProfScope ps("k_mexp_horner", s);
+    bool wave = false;
+    if constexpr (Sh::K == 2048 && MN2::TPI == 16) {
+      // small batches: one 16-wave block per column (latency; k_mexp_horner_wave)
+      static const bool on = [] {
+        const char* e = getenv("XHE_MEXP_WAVE");
+        return !(e && e[0] == '0');
+      }();
+      if (on && ncols <= 4096) {
+        hipLaunchKernelGGL((k_mexp_horner_wave<154, 16>), dim3((unsigned)ncols), dim3(1024), 0, s, k->kd, P, nwin, c,
+                           ncols, out);
+        wave = true;
+      }
+    }
+    if (!wave)
+      hipLaunchKernelGGL(k_mexp_horner<MN2>, blocks(ncols), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, P, nwin, c, ncols,
+                         sq, out);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipStreamSynchronize(s));
-  (void)hipFree(tab);
-  (void)hipFree(P);
-  (void)hipFree(sq);
+  (void)hipFreeAsync(tab, s);
+  (void)hipFreeAsync(P, s);
+  (void)hipFreeAsync(sq, s);
 }
 
 template <class Sh>
@@ -1514,8 +1598,8 @@ void dec_pmd_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chu
   HIPCHK(hipGetLastError());
   {
     ProfScope ps("k_dec_pow", s);
-    hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3(pow_blocks, 2), dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N,
-                       k->kd.pm1_words, k->kd.pm1_bits, k->kd.qm1_words, k->kd.qm1_bits, n, st, ws);
+    hipLaunchKernelGGL((k_dec_pmd_pow<37>), dim3(pow_blocks, 2), dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, 0, n,
+                       st, ws);
     HIPCHK(hipGetLastError());
   }
   hipLaunchKernelGGL((k_dec_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
@@ -1542,7 +1626,7 @@ template <class Sh>
 void dec_pmdx_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chunk, uint32_t* mrows,
                      hipStream_t s) {
   using DO = typename Sh::PDXO;  // conversions (register room)
-  using DP = typename Sh::PDX;   // the exponentiation
+  using DP = typename Sh::PDXO;  // the exponentiation (2 lanes spill 70 VGPRs in pmdx_pow_uniform at 3072)
   using MP2L = typename Sh::MP2L;
   using MP = typename Sh::MP;
   constexpr int RW = Sh::RW, NWH = Sh::K / 64;

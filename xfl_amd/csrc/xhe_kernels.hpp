@@ -108,6 +108,10 @@ struct KeyDev {
   // ---- one-wave decrypt exponentiation (k_dec_wave, 2048-bit keys): the
   // full Montgomery inverse -P^-2 mod R of the MP2 shape (R = 2^(28*74))
   const uint32_t *p2_nprime, *q2_nprime;
+  // ---- one-block Horner of the mat-vec mod n^2 (k_mexp_horner_wave, 2048-bit
+  // keys): n^2 in 154 limbs of 27 bits (R_w = 2^4158), -n^-2 mod R_w and
+  // C = R_w^2 R_X^-1 mod n^2 (R_X = 2^(27*160): the 16-lane shape's R)
+  const uint32_t *n2w_N, *n2w_np, *n2w_C, *n2w_R2;  // (R2: R_w^2 mod n^2, k_mulmod_wave)
 };
 
 // ============================================================== encode
@@ -1199,13 +1203,13 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_
                                        2 * q + 1 < KP ? a[2 * q + 1] : 0u, 2 * q + 1 < KP ? c[2 * q + 1] : 0u);
 }
 
-// st <- st^E_P per prime: E = P - 1 (decrypt) or e_P = n mod phi(P^2)
-// (private non-DJN obfuscator, paillier.py:214-227)
+// st <- st^E_P per prime: E = P - 1 (decrypt, mode 0) or e_P = n mod
+// phi(P^2) (mode 1: the private non-DJN obfuscator, paillier.py:214-227).
+// The exponent is picked from the key inside (4 more pointer/int arguments
+// spill SGPRs in this register-bound kernel).
 template <int KP>
 __global__ void __launch_bounds__(128, 2) k_dec_pmd_pow(KeyDev key, const uint32_t* __restrict__ Pp,
-                                                        const uint32_t* __restrict__ Pq,
-                                                        const uint32_t* __restrict__ ex_p, int bits_p,
-                                                        const uint32_t* __restrict__ ex_q, int bits_q, int64_t count,
+                                                        const uint32_t* __restrict__ Pq, int mode, int64_t count,
                                                         uint4* __restrict__ st, uint4* __restrict__ ws) {
   using D = PMD<KP>;
   constexpr int NQ = D::NQ;
@@ -1215,8 +1219,8 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_pow(KeyDev key, const uint32
   const uint32_t* tcg = prime ? key.topc_q : key.topc_p;
   if (threadIdx.x < KP) topc[threadIdx.x] = tcg[threadIdx.x];
   __syncthreads();
-  const uint32_t* ex = prime ? ex_q : ex_p;
-  const int ebits = prime ? bits_q : bits_p;
+  const uint32_t* ex = mode ? (prime ? key.eq_words : key.ep_words) : (prime ? key.qm1_words : key.pm1_words);
+  const int ebits = mode ? (prime ? key.eq_bits : key.ep_bits) : (prime ? key.qm1_bits : key.pm1_bits);
   // 32-bit indices (count < 2^31 per launch), per-lane addresses formed at
   // use: the product needs every register it can get
   const int G = (int)(gridDim.x * blockDim.x);
@@ -2361,6 +2365,48 @@ __global__ void __launch_bounds__(256, 2) k_mexp_tab(KeyDev key, const uint32_t*
     M.reduce_once(b);
     M.store_row(b, t + (size_t)d * MN2::S4);
   }
+}
+
+// The same tables by levels of entries (one launch per level, lvl = 1..c):
+// level 1 writes base^0, base^1 and base^2; level l >= 2 writes the entries
+// (2^(l-1), 2^l) as tab[2^(l-1)] tab[r] and (l < c) tab[2^l] = tab[2^(l-1)]^2,
+// one product per lane group - a chain of c + 1 products per base instead of
+// the 2^c - 2 of k_mexp_tab (the mat-vec of a small batch is latency-bound).
+template <class MN2>
+__global__ void __launch_bounds__(256, 2) k_mexp_tab_lvl(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                         const uint32_t* __restrict__ bases, int64_t nbases, int c,
+                                                         int lvl, uint32_t* __restrict__ tab) {
+  const int64_t gi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  MN2 M;
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
+  uint32_t b[MN2::L];
+  if (lvl <= 1) {
+    if (gi >= nbases) return;
+    uint32_t* t = tab + ((size_t)gi << c) * MN2::S4;
+    M.load_row(b, n2dev<MN2>(key).R1);
+    M.reduce_once(b);
+    M.store_row(b, t);  // base^0 = R
+    M.load_words(b, bases + (size_t)gi * key.n2w, key.n2w);
+    M.mul(b, ARow{n2dev<MN2>(key).R2});
+    M.reduce_once(b);
+    M.store_row(b, t + MN2::S4);
+    if (c >= 2) {
+      wave_sync_mem_();
+      M.mul(b, ARow{t + MN2::S4});
+      M.reduce_once(b);
+      M.store_row(b, t + 2 * MN2::S4);
+    }
+    return;
+  }
+  const int64_t h = (int64_t)1 << (lvl - 1);
+  const int64_t per = lvl < c ? h : h - 1;  // r = 1..per (r = h: the square)
+  const int64_t bi = gi / per, r = gi - bi * per + 1;
+  if (bi >= nbases) return;
+  uint32_t* t = tab + ((size_t)bi << c) * MN2::S4;
+  M.load_row(b, t + h * MN2::S4);
+  M.mul(b, ARow{t + r * MN2::S4});
+  M.reduce_once(b);
+  M.store_row(b, t + (h + r) * MN2::S4);
 }
 
 // One lane group per (segment s = j*nwin + w, chunk t): the product of the
