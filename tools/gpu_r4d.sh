@@ -6,4 +6,5 @@ TAG=${1:-r4d}
 mkdir -p gpurun_out/$TAG
 bash tools/profile_box.sh "$TAG/prof" || exit $?
 bash tools/pmc_ops.sh "$TAG/ops" || exit $?
+bash tools/gpu_round.sh "$TAG" lrtrace || exit $?
 echo "r4d done"

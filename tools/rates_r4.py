@@ -6,11 +6,13 @@ process, so each side of an A/B is its own process):
   public DJN encrypt, 2048 bits (w16)   $XHE_NDIG_PUB=0  -> k_djn_pub (Montgomery n^2 tables)
   decrypt, 3072 / 4096 bits (batches)   $XHE_DEC_PMDX=0  -> k_dec_pow 4-lane (Montgomery)
   ciphertext add / 1 M-element sum      (no switch: the round-4 product counts)
+  LR-shaped latency ops (B = 64, D = 15) $XHE_MEXP_WAVE=0 / $XHE_ADD_WAVE=0 -> the 16-lane
+                                        Horner / aligned add instead of one 16-wave block each
 
 Each rate comes with a checksum of the outputs so the two sides can be
 compared for equality.
 
-    python tools/rates_r4.py [--only nodjn,pub,dec3072,dec4096,add,sum] > out.jsonl
+    python tools/rates_r4.py [--only nodjn,pub,dec3072,dec4096,add,sum,pubnodjn,lr,matvec] > out.jsonl
 """
 import argparse
 import hashlib
@@ -51,7 +53,7 @@ def _rand_words(rng, n, words, top_bits=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="nodjn,pub,dec3072,dec4096,add,sum,pubnodjn,matvec")
+    ap.add_argument("--only", default="nodjn,pub,dec3072,dec4096,add,sum,pubnodjn,lr,matvec")
     args = ap.parse_args()
     only = set(args.only.split(","))
     import torch
@@ -109,7 +111,7 @@ def main():
                                                            segh.ctypes.data_as(ctypes.c_void_p), nb, oh.data_ptr(), s)), 3)
                 out({"op": "hist_256x100k_2048", "n": 100_000, "ms": t * 1e3, "sum": _sum(oh)})
         del dk
-    if "pubnodjn" in only or "matvec" in only:
+    if "pubnodjn" in only or "matvec" in only or "lr" in only:
         dk = nat.DeviceKey(2048, n, None, None, None, device=0)
         if "pubnodjn" in only:
             N = 65536
@@ -118,6 +120,27 @@ def main():
             ct = torch.empty((N, dk.n2w), dtype=torch.int32, device="cuda")
             t = _timed(lambda: nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), r.data_ptr(), N, ct.data_ptr(), s)), 2)
             out({"op": "encrypt_public_nodjn_2048", "n": N, "per_s": N / t, "ms": t * 1e3, "sum": _sum(ct)})
+        if "lr" in only:
+            # the LR step's latency-bound shapes (B = 64, D = 15): aligned add of
+            # 15 ciphertexts with a 50-step gap (+ noise), mat-vec 64 x 15 at 70 bits
+            Ns = 15
+            a_ = _rand_words(rng, Ns, dk.n2w, 30)
+            b_ = _rand_words(rng, Ns, dk.n2w, 30)
+            ea_ = torch.full((Ns,), -60, dtype=torch.int32, device="cuda")
+            eb_ = torch.full((Ns,), -10, dtype=torch.int32, device="cuda")
+            o_ = torch.empty_like(a_)
+            eo_ = torch.empty_like(ea_)
+            t = _timed(lambda: nat.check(L.xhe_mulmod(dk.handle, a_.data_ptr(), ea_.data_ptr(), b_.data_ptr(),
+                                                      eb_.data_ptr(), Ns, 50, o_.data_ptr(), eo_.data_ptr(), s)), 5)
+            out({"op": "add_aligned_15_d50", "ms": t * 1e3, "sum": _sum(o_)})
+            B, D, kb = 64, 15, 70
+            bases = _rand_words(rng, B, dk.n2w, 30)
+            idx = torch.from_numpy(np.tile(np.arange(B, dtype=np.int32), (D, 1))).cuda()
+            kx = _rand_words(rng, D * B, 3, kb - 64)
+            mv = torch.empty((D, dk.n2w), dtype=torch.int32, device="cuda")
+            t = _timed(lambda: nat.check(L.xhe_multiexp(dk.handle, bases.data_ptr(), B, idx.data_ptr(), kx.data_ptr(),
+                                                        3, kb, D, B, 0, mv.data_ptr(), s)), 5)
+            out({"op": "matvec_64x15_70bit", "ms": t * 1e3, "sum": _sum(mv)})
         if "matvec" in only:
             # the bench's mat-vec: 2048 ciphertext bases x 15 columns, 53-bit exponents
             B, D, kb = 2048, 15, 53
