@@ -1300,6 +1300,47 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
     offs.push_back(tot);
     tot += (size_t)S4 * n;
   }
+  if constexpr (Sh::K == 2048 && MN2::TPI == 16) {  // (a 1024-thread block: the 16-lane 2048-bit shape's registers)
+  if (count <= 256) {
+    // small batch: one block per sweep (k_tree_up_block / k_tree_down_block)
+    const int nlev = (int)sizes.size();
+    std::vector<int64_t> plan(2 * nlev);
+    for (int l = 0; l < nlev; ++l) {
+      plan[l] = (int64_t)offs[l];
+      plan[nlev + l] = sizes[l];
+    }
+    uint32_t *lv = nullptr, *inv = nullptr, *wds = nullptr;
+    int64_t* dplan = nullptr;
+    HIPCHK(hipMallocAsync((void**)&lv, tot * 4, s));
+    HIPCHK(hipMallocAsync((void**)&inv, tot * 4, s));
+    HIPCHK(hipMallocAsync((void**)&wds, (size_t)2 * k->n2w * 4, s));
+    HIPCHK(hipMallocAsync((void**)&dplan, plan.size() * 8, s));
+    HIPCHK(hipMemcpyAsync(dplan, plan.data(), plan.size() * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_tree_up_block<MN2>, dim3(1), dim3(1024), 0, s, k->kd, n2h<MN2>(k).N, c, count, lv, dplan,
+                       dplan + nlev, nlev, wds);
+    HIPCHK(hipGetLastError());
+    std::vector<uint32_t> root(k->n2w), yinv(k->n2w);
+    HIPCHK(hipMemcpyAsync(root.data(), wds, (size_t)k->n2w * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));  // (plan and root copies done)
+    if (!modinv_words(root.data(), k->n2_host.data(), k->n2w, yinv.data())) {
+      (void)hipFreeAsync(lv, s);
+      (void)hipFreeAsync(inv, s);
+      (void)hipFreeAsync(wds, s);
+      (void)hipFreeAsync(dplan, s);
+      return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
+    }
+    HIPCHK(hipMemcpyAsync(wds + k->n2w, yinv.data(), (size_t)k->n2w * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_tree_down_block<MN2>, dim3(1), dim3(1024), 0, s, k->kd, n2h<MN2>(k).N, wds + k->n2w, lv, inv,
+                       dplan, dplan + nlev, nlev, out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // yinv is host memory of this frame
+    (void)hipFreeAsync(lv, s);
+    (void)hipFreeAsync(inv, s);
+    (void)hipFreeAsync(wds, s);
+    (void)hipFreeAsync(dplan, s);
+    return XHE_OK;
+  }
+  }
   uint32_t *lv = nullptr, *inv = nullptr, *scr = nullptr;
   int32_t* st = nullptr;
   HIPCHK(hipMallocAsync((void**)&lv, tot * 4, s));
@@ -1358,7 +1399,9 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
 // empty segment yields the Montgomery one.
 template <class Sh, class MN2 = typename Sh::MN2>
 uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::vector<int64_t> seg, hipStream_t s,
-                          bool raw = false) {
+                          bool raw = false, const uint32_t* words = nullptr) {
+  // words: raw input as ciphertext words ([count][n2w]) instead of rows
+  // (the first level unpacks them itself; rows is then unused)
   const int S4 = MN2::S4;
   const int64_t nseg = (int64_t)seg.size() - 1;
   // Lane groups the chip holds at 2 waves per SIMD: while a level has at least
@@ -1368,14 +1411,19 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
   // (log4 levels x 4 products, against log32 levels x 32).
   constexpr int64_t kFill = 131072 / MN2::TPI;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
-  // plan every level on the host first: the chunk boundaries of all levels go
-  // up in one copy, and the levels run back to back without a host sync
+  // segments of one length (the mat-vec): the chunks are computed in the
+  // kernel, no plan upload and no host sync
+  bool uniform = nseg > 0;
+  for (int64_t i = 1; i < nseg && uniform; ++i) uniform = seg[i + 1] - seg[i] == seg[1] - seg[0];
+  uniform = uniform && seg[1] - seg[0] > 0;
+  // plan every level on the host first: (first, stride, count) of every chunk
+  // of every level go up in one copy, and the levels run back to back
   struct Level {
-    size_t cb_off;
-    int64_t n_in, n_out;
+    size_t plan_off;
+    int64_t n_in, n_out, seg_len, ncs;
     bool raw;
   };
-  std::vector<int64_t> all_cb;
+  std::vector<int64_t> all;
   std::vector<Level> plan;
   int64_t n_cur = count;
   bool first = true;
@@ -1389,36 +1437,52 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
     if (ones && !(first && raw)) break;  // (plain rows still need Montgomery form)
     const int64_t C = (first && raw) || n_cur / kRawChunk >= kFill ? kRawChunk : 4;
     std::vector<int64_t> nseg_b{0};
-    const size_t off = all_cb.size();
-    all_cb.push_back(0);
-    for (int64_t i = 0; i < nseg; ++i) {
-      const int64_t len = seg[i + 1] - seg[i];
-      const int64_t nch = std::max<int64_t>(1, (len + C - 1) / C);  // an empty segment: one (empty) chunk
-      for (int64_t t = 0; t < nch; ++t) all_cb.push_back(std::min(seg[i + 1], seg[i] + (t + 1) * C));
-      nseg_b.push_back(nseg_b.back() + nch);
+    const size_t off = all.size();
+    int64_t seg_len = 0, ncs = 0;
+    if (uniform) {
+      seg_len = seg[1] - seg[0];
+      ncs = (seg_len + C - 1) / C;
+      for (int64_t i = 0; i < nseg; ++i) nseg_b.push_back(nseg_b.back() + ncs);
+    } else {
+      for (int64_t i = 0; i < nseg; ++i) {
+        const int64_t len = seg[i + 1] - seg[i];
+        const int64_t nch = std::max<int64_t>(1, (len + C - 1) / C);  // an empty segment: one (empty) chunk
+        for (int64_t t = 0; t < nch; ++t) {
+          all.push_back(seg[i] + t);
+          all.push_back(nch);
+          all.push_back(t < len ? (len - t + nch - 1) / nch : 0);
+        }
+        nseg_b.push_back(nseg_b.back() + nch);
+      }
     }
-    const int64_t n_out = (int64_t)(all_cb.size() - off) - 1;
-    plan.push_back({off, n_cur, n_out, first && raw});
+    const int64_t n_out = nseg_b.back();
+    plan.push_back({off, n_cur, n_out, seg_len, ncs, first && raw});
     n_cur = n_out;
     seg.swap(nseg_b);
     first = false;
   }
   if (plan.empty()) return rows;  // already one Montgomery row per segment
-  int64_t* dcb = nullptr;
-  HIPCHK(hipMallocAsync((void**)&dcb, all_cb.size() * 8, s));
-  HIPCHK(hipMemcpyAsync(dcb, all_cb.data(), all_cb.size() * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));  // all_cb is host memory of this frame (one sync per call)
+  int64_t* dplan = nullptr;
+  if (!all.empty()) {
+    HIPCHK(hipMallocAsync((void**)&dplan, all.size() * 8, s));
+    HIPCHK(hipMemcpyAsync(dplan, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // `all` is host memory of this frame (one sync per call)
+  }
   uint32_t* cur = rows;
   for (const Level& L : plan) {
     uint32_t* nxt = nullptr;
     HIPCHK(hipMallocAsync((void**)&nxt, (size_t)S4 * std::max<int64_t>(L.n_out, 1) * 4, s));
-    hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(L.n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, L.n_in,
-                       dcb + L.cb_off, L.n_out, nxt, L.raw ? 1 : 0);
+    if (L.raw && words)
+      hipLaunchKernelGGL((k_chunk_prod_words<MN2, Sh::RW2>), blocks(L.n_out), dim3(256), 0, s, k->kd,
+                         n2h<MN2>(k).N, words, uniform ? nullptr : dplan + L.plan_off, L.seg_len, L.ncs, L.n_out, nxt);
+    else
+      hipLaunchKernelGGL(k_chunk_prod<MN2>, blocks(L.n_out), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, L.n_in,
+                         uniform ? nullptr : dplan + L.plan_off, L.seg_len, L.ncs, L.n_out, nxt, L.raw ? 1 : 0);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipFreeAsync(cur, s));
+    if (cur) HIPCHK(hipFreeAsync(cur, s));
     cur = nxt;
   }
-  HIPCHK(hipFreeAsync(dcb, s));
+  if (dplan) HIPCHK(hipFreeAsync(dplan, s));
   return cur;
 }
 
@@ -1430,20 +1494,28 @@ void segprod_impl(const xhe_key* k, const uint32_t* c, const int32_t* d, int dma
   const int S4 = MN2::S4;
   auto blocks = [&](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n * MN2::TPI + 255) / 256)); };
   uint32_t *rows = nullptr, *sq = nullptr;
-  HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
-  HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
-  if (count > 0) {
+  // no alignment anywhere: the first level reads the ciphertext words itself
+  // ($XHE_SUM_WORDS=0: the k_align_mont transpose first, A/B)
+  static const bool words_on = [] {
+    const char* e = getenv("XHE_SUM_WORDS");
+    return !(e && e[0] == '0');
+  }();
+  const bool direct = count > 0 && (dmax == 0 || !d) && words_on;
+  if (!direct) {
+    HIPCHK(hipMallocAsync((void**)&rows, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+    HIPCHK(hipMallocAsync((void**)&sq, (size_t)S4 * std::max<int64_t>(count, 1) * 4, s));
+  }
+  if (count > 0 && !direct) {
     hipLaunchKernelGGL(k_align_mont<MN2>, blocks(count), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, c, d, count, dmax,
                        rows, sq);
     HIPCHK(hipGetLastError());
   }
-  uint32_t* cur =
-      reduce_segments<Sh, MN2>(k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s, true);
+  uint32_t* cur = reduce_segments<Sh, MN2>(
+      k, rows, count, std::vector<int64_t>(seg_begin_host, seg_begin_host + nseg + 1), s, true, direct ? c : nullptr);
   hipLaunchKernelGGL(k_from_mont_rows<MN2>, blocks(nseg), dim3(256), 0, s, k->kd, n2h<MN2>(k).N, cur, nseg, out);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
-  (void)hipFreeAsync(cur, s);
-  (void)hipFreeAsync(sq, s);
+  (void)hipFreeAsync(cur, s);  // stream-ordered: no host sync (the output is ready in stream order)
+  if (sq) (void)hipFreeAsync(sq, s);
 }
 
 // Window bits for a multi-exponentiation: minimise table products
@@ -1521,8 +1593,7 @@ void multiexp_impl(const xhe_key* k, const uint32_t* bases, int64_t nbases, cons
                          sq, out);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipStreamSynchronize(s));
-  (void)hipFreeAsync(tab, s);
+  (void)hipFreeAsync(tab, s);  // stream-ordered frees: no host sync
   (void)hipFreeAsync(P, s);
   (void)hipFreeAsync(sq, s);
 }

@@ -2215,29 +2215,83 @@ __global__ void __launch_bounds__(256, 2) k_align_mont(KeyDev key, const uint32_
   M.store_strided(b, rows + e, st);
 }
 
-// One reduction level: chunk j multiplies rows [cbeg[j], cbeg[j+1]) (rows
-// [S4][n_in]) into the Montgomery row j of out ([S4][n_out]). raw: the input
-// rows are plain residues and chunks are at most kRawChunk long: L plain
-// residues chain to P R^-(L-1), and one product by R^(L+1) gives P R - one
-// product per element plus one per chunk instead of two per element.
+// One reduction level: chunk j multiplies `count` rows of a segment, the
+// rows first, first + stride, ... (rows [S4][n_in]) into the Montgomery row j
+// of out ([S4][n_out]). Chunks are INTERLEAVED over their segment (chunk t of
+// nch takes rows t, t + nch, ...): at every step neighbouring lane groups
+// read neighbouring columns, one 64-B piece per wave, where contiguous chunks
+// of 32 made every group of a wave read its own cache line (20 GB fetched
+// per 1 M-row level, `profiles/r4/pmc_ops/`). The product is the same residue
+// in any order. plan: (first, stride, count) per chunk; plan == nullptr: every
+// segment has seg_len rows and ncs chunks (the mat-vec's uniform segments, no
+// upload). raw: the input rows are plain residues and count <= kRawChunk: L
+// plain residues chain to P R^-(L-1), and one product by R^(L+1) gives P R -
+// one product per element plus one per chunk instead of two per element.
 template <class MN2>
 __global__ void __launch_bounds__(256, 2) k_chunk_prod(KeyDev key, const uint32_t* __restrict__ Nn2,
                                                        const uint32_t* __restrict__ in, int64_t n_in,
-                                                       const int64_t* __restrict__ cbeg, int64_t n_out,
-                                                       uint32_t* __restrict__ outp, int raw) {
+                                                       const int64_t* __restrict__ plan, int64_t seg_len, int64_t ncs,
+                                                       int64_t n_out, uint32_t* __restrict__ outp, int raw) {
   const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
   if (j >= n_out) return;
+  int64_t first, stride, cnt;
+  if (plan) {
+    first = plan[3 * j];
+    stride = plan[3 * j + 1];
+    cnt = plan[3 * j + 2];
+  } else {
+    const int64_t sg = j / ncs, t = j - sg * ncs;
+    first = sg * seg_len + t;
+    stride = ncs;
+    cnt = t < seg_len ? (seg_len - t + ncs - 1) / ncs : 0;
+  }
   MN2 M;
   M.init(Nn2, n2dev<MN2>(key).n0inv);
   uint32_t b[MN2::L];
-  const int64_t lo = cbeg[j], hi = cbeg[j + 1];
-  if (hi <= lo) {  // empty segment: Montgomery one
+  if (cnt <= 0) {  // empty segment: Montgomery one
     M.load_row(b, n2dev<MN2>(key).R1);
     M.reduce_once(b);
   } else {
-    M.load_strided(b, in + lo, (int)n_in);
-    for (int64_t i = lo + 1; i < hi; ++i) M.mul(b, AStrided{in + i, (int)n_in});
-    if (raw) M.mul(b, ARow{n2dev<MN2>(key).Rpow + (size_t)(hi - lo + 1) * MN2::S4});
+    M.load_strided(b, in + first, (int)n_in);
+    for (int64_t u = 1; u < cnt; ++u) M.mul(b, AStrided{in + first + u * stride, (int)n_in});
+    if (raw) M.mul(b, ARow{n2dev<MN2>(key).Rpow + (size_t)(cnt + 1) * MN2::S4});
+    M.reduce_once(b);
+  }
+  M.store_strided(b, outp + j, (int)n_out);
+}
+
+// The first (raw) level straight from the input ciphertexts ([n][PW] words,
+// element-major) when no element needs alignment: no k_align_mont pass (a
+// 1.2 GB transpose per 1 M elements); the operands are unpacked from their
+// words where they are used (ARowPacked), chunks interleaved as above.
+template <class MN2, int PW>
+__global__ void __launch_bounds__(256, 2) k_chunk_prod_words(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                             const uint32_t* __restrict__ words,
+                                                             const int64_t* __restrict__ plan, int64_t seg_len,
+                                                             int64_t ncs, int64_t n_out, uint32_t* __restrict__ outp) {
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MN2::TPI;
+  if (j >= n_out) return;
+  int64_t first, stride, cnt;
+  if (plan) {
+    first = plan[3 * j];
+    stride = plan[3 * j + 1];
+    cnt = plan[3 * j + 2];
+  } else {
+    const int64_t sg = j / ncs, t = j - sg * ncs;
+    first = sg * seg_len + t;
+    stride = ncs;
+    cnt = t < seg_len ? (seg_len - t + ncs - 1) / ncs : 0;
+  }
+  MN2 M;
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
+  uint32_t b[MN2::L];
+  if (cnt <= 0) {
+    M.load_row(b, n2dev<MN2>(key).R1);
+    M.reduce_once(b);
+  } else {
+    M.load_words(b, words + (size_t)first * PW, PW);
+    for (int64_t u = 1; u < cnt; ++u) M.mul(b, ARowPacked<MN2::W, PW>{words + (size_t)(first + u * stride) * PW});
+    M.mul(b, ARow{n2dev<MN2>(key).Rpow + (size_t)(cnt + 1) * MN2::S4});
     M.reduce_once(b);
   }
   M.store_strided(b, outp + j, (int)n_out);
@@ -2311,6 +2365,95 @@ __global__ void __launch_bounds__(256, 2) k_from_mont_rows(KeyDev key, const uin
   M.mul(b, AOne{});
   M.reduce_once(b);
   store_packed(M, b, rows + e, (int)count, out + (size_t)e * key.n2w, key.n2w);
+}
+
+// Small batches (<= one block of lane groups): the whole up-sweep in ONE
+// launch - to Montgomery rows, every tree level (__syncthreads between
+// levels; the levels' rows in global memory, offsets lvo[l] and sizes lvn[l]
+// host-planned as for k_tree_up) and the root packed to words - and the whole
+// down-sweep in another (root inverse to a row, every level, out of
+// Montgomery form). A batch inversion of the LR step's 64 bases took 16
+// launches of one 16-lane product each (the launch gaps, not the products,
+// were most of its ~0.3 ms).
+template <class MN2>
+__global__ void __launch_bounds__(1024) k_tree_up_block(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                        const uint32_t* __restrict__ c, int64_t count,
+                                                        uint32_t* __restrict__ lv, const int64_t* __restrict__ lvo,
+                                                        const int64_t* __restrict__ lvn, int nlev,
+                                                        uint32_t* __restrict__ root_words) {
+  const int groups = (int)(blockDim.x / MN2::TPI);
+  const int g = (int)(threadIdx.x / MN2::TPI);
+  MN2 M;
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
+  uint32_t b[MN2::L];
+  for (int64_t e = g; e < count; e += groups) {
+    M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
+    M.mul(b, ARow{n2dev<MN2>(key).R2});
+    M.reduce_once(b);
+    M.store_strided(b, lv + e, (int)count);
+  }
+  __syncthreads();
+  for (int l = 1; l < nlev; ++l) {
+    const int64_t n_in = lvn[l - 1], n_out = lvn[l];
+    const uint32_t* in = lv + lvo[l - 1];
+    uint32_t* outp = lv + lvo[l];
+    for (int64_t i = g; i < n_out; i += groups) {
+      M.load_strided(b, in + 2 * i, (int)n_in);
+      if (2 * i + 1 < n_in) {
+        M.mul(b, AStrided{in + 2 * i + 1, (int)n_in});
+        M.reduce_once(b);
+      }
+      M.store_strided(b, outp + i, (int)n_out);
+    }
+    __syncthreads();
+  }
+  if (g == 0) pack_words_<MN2::W, MN2::TPI>(lv + lvo[nlev - 1], 1, MN2::S, root_words, key.n2w);
+}
+
+template <class MN2>
+__global__ void __launch_bounds__(1024) k_tree_down_block(KeyDev key, const uint32_t* __restrict__ Nn2,
+                                                          const uint32_t* __restrict__ y_words,
+                                                          const uint32_t* __restrict__ lv, uint32_t* __restrict__ inv,
+                                                          const int64_t* __restrict__ lvo,
+                                                          const int64_t* __restrict__ lvn, int nlev,
+                                                          uint32_t* __restrict__ out) {
+  const int groups = (int)(blockDim.x / MN2::TPI);
+  const int g = (int)(threadIdx.x / MN2::TPI);
+  MN2 M;
+  M.init(Nn2, n2dev<MN2>(key).n0inv);
+  uint32_t b[MN2::L];
+  if (g == 0) {  // (P R)^-1 words -> P^-1 R (as k_inv_to_row)
+    M.load_words(b, y_words, key.n2w);
+    M.mul(b, ARow{n2dev<MN2>(key).R3});
+    M.reduce_once(b);
+    M.store_strided(b, inv + lvo[nlev - 1], 1);
+  }
+  __syncthreads();
+  for (int l = nlev - 1; l >= 1; --l) {
+    const int64_t n_par = lvn[l], n_child = lvn[l - 1];
+    const uint32_t* pinv = inv + lvo[l];
+    const uint32_t* child = lv + lvo[l - 1];
+    uint32_t* cinv = inv + lvo[l - 1];
+    for (int64_t i = g; i < n_child; i += groups) {
+      M.load_strided(b, pinv + i / 2, (int)n_par);
+      const int64_t sib = i ^ 1;
+      if (sib < n_child) {
+        M.mul(b, AStrided{child + sib, (int)n_child});
+        M.reduce_once(b);
+      }
+      M.store_strided(b, cinv + i, (int)n_child);
+    }
+    __syncthreads();
+  }
+  const int64_t count = lvn[0];
+  for (int64_t e = g; e < count; e += groups) {
+    M.load_strided(b, inv + e, (int)count);
+    M.mul(b, AOne{});
+    M.reduce_once(b);
+    M.store_strided(b, const_cast<uint32_t*>(lv) + e, (int)count);  // the level-0 rows are free now: pack scratch
+    wave_sync_mem_();
+    pack_words_<MN2::W, MN2::TPI>(lv + e, (int)count, MN2::S, out + (size_t)e * key.n2w, key.n2w);
+  }
 }
 
 // Root of the product tree <-> plain words for k_inv_single (one group).
