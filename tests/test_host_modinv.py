@@ -43,3 +43,36 @@ def test_modinv_words_matches_python(harness):
         except ValueError:
             want = "none"
         assert got == want
+
+
+def test_modinv_words_random_sizes(harness):
+    """62-step batches (round 4): random odd moduli of 1..130 words, operands
+    of every size below them (the exact path below 126 bits, the approximate
+    one above, the boundary around 2 words), small and structured operands."""
+    rng = random.Random(12)
+    cases = []
+    for _ in range(1500):
+        nw = rng.choice([1, 2, 3, 4, 5, 8, 16, 33, 64, 96, 128, 130])
+        bits = rng.randrange(max(2, 32 * nw - 40), 32 * nw + 1)
+        m = rng.getrandbits(bits) | 1 | (1 << (bits - 1))
+        kind = rng.randrange(5)
+        if kind == 0:
+            x = rng.randrange(1, m)
+        elif kind == 1:
+            x = rng.randrange(1, min(m, 1 << rng.randrange(1, 130)))
+        elif kind == 2:
+            x = m - rng.randrange(1, min(m, 1 << 20))
+        elif kind == 3:
+            x = (1 << rng.randrange(0, bits - 1)) % m or 1
+        else:
+            x = rng.randrange(1, m) | ((1 << (bits - 1)) - 1) % m or 1
+        cases.append((nw, x, m))
+    inp = "".join(f"{nw} {x:x} {m:x}\n" for nw, x, m in cases)
+    out = subprocess.run([harness], input=inp, capture_output=True, text=True, check=True).stdout.split()
+    assert len(out) == len(cases)
+    for (nw, x, m), got in zip(cases, out):
+        try:
+            want = f"{pow(x, -1, m):0{8 * nw}x}"
+        except ValueError:
+            want = "none"
+        assert got == want, (nw, hex(x), hex(m))

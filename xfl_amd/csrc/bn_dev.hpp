@@ -1001,6 +1001,37 @@ struct Mont {
     for (int j = 0; j < L; ++j)
       if (g * L + j < nlimbs) p[(size_t)(g * L + j) * stride] = b[j];
   }
+  // b (normalised limbs) packed to nwords little-endian 32-bit words straight
+  // from the registers: lane g writes the words that START in its limbs, the
+  // next lane's first two limbs (DPP) complete the last of them - the same
+  // words as store_strided + pack_words_, without the round trip through a
+  // strided row (a write and a read of S4 words per element).
+  XHE_DEV void store_words(const uint32_t (&b)[L], uint32_t* __restrict__ out, int nwords) const {
+    const uint32_t n0 = G::from_next(b[0]);
+    const uint32_t n1 = G::from_next(L > 1 ? b[1] : 0u);
+    store_words_g<0>(b, n0, n1, out, nwords, G::g());
+  }
+  template <int GG>
+  XHE_DEV static void store_words_g(const uint32_t (&b)[L], uint32_t n0, uint32_t n1, uint32_t* __restrict__ out,
+                                    int nwords, int g) {
+    if constexpr (GG < TPI) {
+      if (GG == TPI - 1 || g == GG) {
+        constexpr int b0 = W * L * GG, b1 = W * L * (GG + 1);
+        constexpr int k0 = (b0 + 31) / 32, k1 = (b1 + 31) / 32;
+        auto limb = [&](int x) -> uint64_t {
+          return x < L ? (uint64_t)b[x] : x == L ? (uint64_t)n0 : x == L + 1 ? (uint64_t)n1 : 0ull;
+        };
+#pragma unroll
+        for (int k = k0; k < k1; ++k) {
+          const int bit = 32 * k - b0, jl = bit / W, sh = bit - jl * W;
+          const uint64_t v = limb(jl) | (limb(jl + 1) << W) | (limb(jl + 2) << (2 * W));
+          if (k < nwords) out[k] = (uint32_t)(v >> sh);
+        }
+      } else {
+        store_words_g<GG + 1>(b, n0, n1, out, nwords, g);
+      }
+    }
+  }
   // Store this lane's limbs one per word into an interleaved row.
   XHE_DEV void store_strided(const uint32_t (&b)[L], uint32_t* p, int stride) const {
     p = opaque(p);

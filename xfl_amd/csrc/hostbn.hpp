@@ -271,13 +271,13 @@ inline bool modinv_words_binary(const uint32_t* x32, const uint32_t* m32, int nw
 }
 
 // x^-1 mod m for odd m, x < m: the binary extended GCD with the iterations
-// batched 31 at a time (the approach of T. Pornin, "Optimized Binary GCD for
-// Modular Inversion", 2020). A batch runs on 64-bit approximations of a and b
-// (their low 31 bits, exact, and their top 33 bits at a common position): the
-// parity tests are exact, the comparisons approximate; the batch's 2x2 update
-// matrix (entries <= 2^31) is then applied once to the full-width a, b and to
-// the Bezout cofactors u, v mod m (each divided by 2^31 with one Montgomery
-// step), and a row that came out negative is negated. About 2 len(m) / 31
+// batched KB = 62 at a time (the approach of T. Pornin, "Optimized Binary GCD for
+// Modular Inversion", 2020). A batch runs on 126-bit approximations of a and b
+// (their low KB bits, exact, and their top KB + 2 bits at a common position):
+// the parity tests are exact, the comparisons approximate; the batch's 2x2
+// update matrix (entries <= 2^KB) is then applied once to the full-width a, b
+// and to the Bezout cofactors u, v mod m (each divided by 2^KB with one
+// Montgomery step), and a row that came out negative is negated. About 2 len(m) / KB
 // batches of a few linear passes, instead of ~2 len(m) full-width shift /
 // subtract passes. Returns false when gcd(x, m) != 1; falls back to the plain
 // binary algorithm if the batch budget runs out (never observed).
@@ -314,7 +314,15 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
     u64 lo = w < W ? x[w] : 0, hi = w + 1 < W ? x[w + 1] : 0;
     return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
   };
-  // r = (f x + g y) / 2^31, exact; returns true when negative (r then holds
+  // KB = 62 steps per batch (round 4; was 31): 126-bit approximations (the
+  // low 62 bits exact, the top 64 at a common position) in unsigned
+  // __int128, update factors |f| + |g| <= 2^62 in int64, so the linear passes
+  // below (f x + g y, |.| < 2^126 per word) stay inside __int128: half the
+  // batches of the same passes (4096-bit root inverse 172 -> ~90 us here).
+  constexpr int KB = 62;
+  using u128 = unsigned __int128;
+  const u64 MK = (1ull << KB) - 1;
+  // r = (f x + g y) / 2^KB, exact; returns true when negative (r then holds
   // the magnitude)
   auto lin_shift = [&](int64_t f, const std::vector<u64>& x, int64_t g, const std::vector<u64>& y,
                        std::vector<u64>& r) {
@@ -334,15 +342,14 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
         t[i] = nv;
       }
     }
-    for (int i = 0; i < W; ++i) r[i] = (t[i] >> 31) | (t[i + 1] << 33);
+    for (int i = 0; i < W; ++i) r[i] = (t[i] >> KB) | (t[i + 1] << (64 - KB));
     return neg;
   };
   // -m^-1 mod 2^64 (Newton)
   u64 minv = 1;
   for (int i = 0; i < 6; ++i) minv *= 2 - m[0] * minv;
   const u64 mneg_inv = (u64)0 - minv;
-  const u64 M31 = (1ull << 31) - 1;
-  // r = (f x + g y) 2^-31 mod m, x, y in [0, m)
+  // r = (f x + g y) 2^-KB mod m, x, y in [0, m)
   auto lin_mod = [&](int64_t f, const std::vector<u64>& x, int64_t g, const std::vector<u64>& y,
                      std::vector<u64>& r) {
     i128 c = 0;
@@ -352,7 +359,7 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
       c >>= 64;
     }
     t[W] = (u64)(int64_t)c;
-    const u64 q = (t[0] * mneg_inv) & M31;  // t + q m = 0 (mod 2^31)
+    const u64 q = (t[0] * mneg_inv) & MK;  // t + q m = 0 (mod 2^KB)
     unsigned __int128 cc = 0;
     i128 sc = 0;
     for (int i = 0; i < W; ++i) {
@@ -362,9 +369,9 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
     }
     sc = (i128)(int64_t)t[W] + (i128)(u64)cc;
     t[W] = (u64)sc;
-    // shift right 31 (arithmetic), value in (-3m, 3m)
-    for (int i = 0; i < W; ++i) r[i] = (t[i] >> 31) | (t[i + 1] << 33);
-    int64_t top = (int64_t)t[W] >> 31;  // sign word of the shifted value (0 or -1)
+    // shift right KB (arithmetic), value in (-3m, 3m)
+    for (int i = 0; i < W; ++i) r[i] = (t[i] >> KB) | (t[i + 1] << (64 - KB));
+    int64_t top = (int64_t)t[W] >> KB;  // sign word of the shifted value (0 or -1)
     // bring into [0, m)
     for (int it = 0; it < 4 && top < 0; ++it) {  // add m
       unsigned __int128 k2 = 0;
@@ -385,7 +392,7 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
     }
   };
   std::vector<u64> na(W), nb(W), nu(W), nv(W);
-  const int max_batches = (2 * 64 * W) / 31 + 16;
+  const int max_batches = (2 * 64 * W) / KB + 16;
   for (int batch = 0; batch < max_batches; ++batch) {
     if (is_zero(a)) {
       // b = gcd(x, m)
@@ -395,18 +402,18 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
       for (int i = 0; i < nw32; ++i) out32[i] = (uint32_t)(v[i / 2] >> (32 * (i & 1)));
       return true;
     }
-    const int n = std::max(std::max(bitlen(a), bitlen(b)), 64);
-    u64 xa, xb;
-    if (n <= 64) {
-      xa = a[0];
-      xb = b[0];
+    const int n = std::max(std::max(bitlen(a), bitlen(b)), 128);
+    u128 xa, xb;
+    if (n <= 2 * KB + 2) {  // exact
+      xa = (u128)a[0] | ((u128)(W > 1 ? a[1] : 0) << 64);
+      xb = (u128)b[0] | ((u128)(W > 1 ? b[1] : 0) << 64);
     } else {
-      xa = (bits_at(a, n - 33) << 31) | (a[0] & M31);
-      xb = (bits_at(b, n - 33) << 31) | (b[0] & M31);
+      xa = ((u128)bits_at(a, n - 64) << KB) | (a[0] & MK);
+      xb = ((u128)bits_at(b, n - 64) << KB) | (b[0] & MK);
     }
     int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
-    for (int j = 0; j < 31; ++j) {
-      if (xa & 1) {
+    for (int j = 0; j < KB; ++j) {
+      if ((uint64_t)xa & 1) {
         if (xa < xb) {
           std::swap(xa, xb);
           std::swap(f0, f1);
@@ -417,7 +424,7 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
         g0 -= g1;
       }
       xa >>= 1;
-      f1 *= 2;  // |f1|, |g1| <= 2^31: no overflow (a shift of a negative value would be UB)
+      f1 *= 2;  // |f1|, |g1| <= 2^62: no overflow (a shift of a negative value would be UB)
       g1 *= 2;
     }
     if (lin_shift(f0, a, g0, b, na)) {

@@ -1733,11 +1733,20 @@ __global__ void __launch_bounds__(256, 2) k_crt_dec(KeyDev key, const uint32_t* 
 
 // ============================================================== mod n^2
 // Helpers shared by the n^2 kernels (shape MN2, usually TPI = 4).
+#ifndef XHE_STORE_DIRECT
+#define XHE_STORE_DIRECT 1  // store_packed straight from the registers (Mont::store_words); 0: via the strided row
+#endif
 template <class M_>
 XHE_DEV void store_packed(const M_& M, const uint32_t (&b)[M_::L], uint32_t* row, int st, uint32_t* out, int nwords) {
+#if XHE_STORE_DIRECT
+  (void)row;
+  (void)st;
+  M.store_words(b, out, nwords);
+#else
   M.store_strided(b, row, st);
   wave_sync_mem_();
   pack_words_<M_::W, M_::TPI>(row, st, M_::S, out, nwords);
+#endif
 }
 
 // 4-bit fixed-window power of the Montgomery residue in b. Digits come from
