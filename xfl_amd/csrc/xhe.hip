@@ -400,7 +400,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
     size_t topc_p = 0, topc_q = 0;
-    size_t nprime_p2 = 0, nprime_q2 = 0;
+    size_t nprime_p2 = 0, nprime_q2 = 0, nprime37_p = 0, nprime37_q = 0;
     ModOff xd[2];
     size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
     size_t xdw[2] = {0, 0}, xhpR[2] = {0, 0};
@@ -495,6 +495,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       };
       o.topc_p = topc(P);
       o.topc_q = topc(Q);
+      // -P^-1 mod R for the whole-wave digit kernels (WaveDig)
+      o.nprime37_p = bl.put(sub(T, modinv(mod(P, T), T)).to_limbs(28, 37));
+      o.nprime37_q = bl.put(sub(T, modinv(mod(Q, T), T)).to_limbs(28, 37));
     }
 #endif
 #if XHE_PMDX
@@ -636,6 +639,8 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     if (K == 2048) {
       kd.topc_p = B + o.topc_p;
       kd.topc_q = B + o.topc_q;
+      kd.p_nprime37 = B + o.nprime37_p;
+      kd.q_nprime37 = B + o.nprime37_q;
     }
 #endif
 #if XHE_PMDX
@@ -861,6 +866,18 @@ void crt_enc_launch(const xhe_key* k, int64_t n, uint32_t* ws, uint32_t* ct, hip
   HIPCHK(hipGetLastError());
 }
 
+// Whole-wave digit kernels for the smallest 2048-bit batches (k_djn_wavedig
+// up to kEncWaveMax elements, k_dec_wavedig for the decrypt's wave regime);
+// $XHE_WAVEDIG=0 keeps k_djn_pmd<16> / k_dec_wave (A/B).
+constexpr int64_t kEncWaveMax = 256;
+bool wavedig_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_WAVEDIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // lanes per element of k_djn_pmd: 16 up to 2 k elements, 4 up to 16 k, else
 // 1 (the chip holds ~128 k one-lane residues: 2 waves x 1024 SIMDs x 64);
 // $XHE_PMD_SPLIT pins it (1, 4 or 16)
@@ -886,6 +903,26 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     int blocks = (int)((n * MP2::TPI + 255) / 256);
 #if XHE_PMD && XHE_LDS_ROWS
     if constexpr (Sh::K == 2048) {
+      if (k->kd.pmd && n <= kEncWaveMax && wavedig_on()) {
+        // the smallest batches: one 4-wave block per (element, prime), the
+        // fixed-base products as whole-wave digit products (k_djn_wavedig),
+        // then (1 + n m) folded on the way to the rows (k_nodjn_pmd_out)
+        using WD = WaveDig<37, 4>;
+        uint4* st = nullptr;
+        ws_alloc((void**)&st, (size_t)2 * WD::NQ * n * sizeof(uint4), s);
+        {
+          ProfScope ps("k_djn_pmd", s);
+          hipLaunchKernelGGL((k_djn_wavedig<37, 4, Sh::RW>), dim3((unsigned)n, 2), dim3(256), 0, s, k->kd,
+                             r + (size_t)off * k->rand_words, k->rand_words, n, st);
+          HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL((k_nodjn_pmd_out<MP2, 37>), dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
+                           k->kd.p.N, k->kd.q.N, k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, n, st, ws);
+        HIPCHK(hipGetLastError());
+        ws_free(st, s);
+        crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
+        continue;
+      }
       if (k->kd.pmd) {
         ProfScope ps("k_djn_pmd", s);
         // small batches split each element's windows over G lanes (latency:
@@ -1771,10 +1808,34 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
 #endif
     if (tpi == 64) {
       if constexpr (wave_ok) {
+#if XHE_PMD && XHE_LDS_ROWS
+        if (wavedig_on()) {
+          // digits: k_dec_pmd_in (c -> digits), x^(P-1) on whole-wave digit
+          // products (k_dec_wavedig), k_dec_pmd_out (-> X_P rows)
+          constexpr int NQ = PMD<37>::NQ;
+          uint4* st = nullptr;
+          ws_alloc((void**)&st, (size_t)2 * NQ * n * sizeof(uint4), s);
+          const dim3 g1((unsigned)((n + 127) / 128), 2);
+          hipLaunchKernelGGL((k_dec_pmd_in<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                             k->kd.q2.N, cto, k->n2w, n, st);
+          HIPCHK(hipGetLastError());
+          {
+            ProfScope ps("k_dec_wave", s);
+            hipLaunchKernelGGL((k_dec_wavedig<37, 4>), dim3((unsigned)n, 2), dim3(256), 0, s, k->kd, n, st);
+            HIPCHK(hipGetLastError());
+          }
+          hipLaunchKernelGGL((k_dec_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
+                             k->kd.q2.N, n, st, (int)MP2::S4, xrows);
+          HIPCHK(hipGetLastError());
+          ws_free(st, s);
+        } else
+#endif
+        {
         static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave shares the MP2 limbs");
         ProfScope ps("k_dec_wave", s);
         hipLaunchKernelGGL((k_dec_wave<74, XHE_DEC_NWV>), dim3((unsigned)n, 2), dim3(64 * XHE_DEC_NWV), 0, s, k->kd, cto, n, (int)MP2::S4, xrows);
         HIPCHK(hipGetLastError());
+        }
       }
     } else if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
     else if (tpi == 4) dec_pow_launch<typename Sh::MP2L, 1, MP2>(k, cto, n, chunk, xrows, s);

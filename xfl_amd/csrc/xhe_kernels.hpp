@@ -112,6 +112,9 @@ struct KeyDev {
   // keys): n^2 in 154 limbs of 27 bits (R_w = 2^4158), -n^-2 mod R_w and
   // C = R_w^2 R_X^-1 mod n^2 (R_X = 2^(27*160): the 16-lane shape's R)
   const uint32_t *n2w_N, *n2w_np, *n2w_C, *n2w_R2;  // (R2: R_w^2 mod n^2, k_mulmod_wave)
+  // ---- Montgomery digits on whole waves (WaveDig, 2048-bit keys): -P^-1 mod
+  // R (R = 2^(28*37)) as 37 limbs, per prime
+  const uint32_t *p_nprime37, *q_nprime37;
 };
 
 // ============================================================== encode
