@@ -62,3 +62,25 @@ def test_resident_batches_capped_by_hbm_budget(monkeypatch):
     assert resident.device_for(priv, -1) == 0  # existing arrays: no count, no cap
     monkeypatch.setenv("XHE_RESIDENT", "0")
     assert resident.device_for(priv, -1, 1, per) is None
+
+
+def test_small_resident_batches_skip_the_hbm_query(monkeypatch):
+    """Batches below RESIDENT_QUERY_MIN take the resident path without
+    querying torch's allocator (a per-call cost on the latency-bound LR
+    shapes); larger ones still check the budget."""
+    from tests.conftest import load_fixture
+    from xfl_amd import _native
+    from xfl_amd.paillier import resident
+
+    monkeypatch.setattr(resident, "available", lambda: True)
+    for v in ("XHE_RESIDENT", "XHE_DEVICES", "LOCAL_RANK", "XHE_RESIDENT_MAX_BYTES"):
+        monkeypatch.delenv(v, raising=False)
+    priv, _ = C.ctxs(load_fixture("paillier_2048_djn.json"))
+    queried = []
+    monkeypatch.setattr(_native, "device_free_bytes", lambda dev: queried.append(dev) or 0)
+    per = 4 * 128 + 16
+    assert resident.device_for(priv, -1, 64, per) == 0
+    assert queried == []
+    big = resident.RESIDENT_QUERY_MIN // per + 1
+    assert resident.device_for(priv, -1, big, per) is None  # 0 bytes free
+    assert queried == [0]

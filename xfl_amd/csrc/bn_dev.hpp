@@ -1006,30 +1006,37 @@ struct Mont {
   // next lane's first two limbs (DPP) complete the last of them - the same
   // words as store_strided + pack_words_, without the round trip through a
   // strided row (a write and a read of S4 words per element).
+  // The code is the same for every lane: the lane's bits (and the next
+  // lane's first two limbs) packed into local words u[] at compile-time
+  // positions, then one funnel shift by the lane's runtime bit offset per
+  // output word and a predicated store. (A first form branched per lane
+  // position with compile-time offsets; the compiler merged the branches'
+  // last stores into a shared tail and put one operand copy on the wrong
+  // lane's path - wrong top words of the 3072-bit mod-p^2 outputs, DESIGN.md
+  // round 4.)
   XHE_DEV void store_words(const uint32_t (&b)[L], uint32_t* __restrict__ out, int nwords) const {
+    constexpr int LB = L * W;                // bits per lane
+    constexpr int NWM = (LB + 31) / 32 + 1;  // bound on the words starting in one lane
     const uint32_t n0 = G::from_next(b[0]);
     const uint32_t n1 = G::from_next(L > 1 ? b[1] : 0u);
-    store_words_g<0>(b, n0, n1, out, nwords, G::g());
-  }
-  template <int GG>
-  XHE_DEV static void store_words_g(const uint32_t (&b)[L], uint32_t n0, uint32_t n1, uint32_t* __restrict__ out,
-                                    int nwords, int g) {
-    if constexpr (GG < TPI) {
-      if (GG == TPI - 1 || g == GG) {
-        constexpr int b0 = W * L * GG, b1 = W * L * (GG + 1);
-        constexpr int k0 = (b0 + 31) / 32, k1 = (b1 + 31) / 32;
-        auto limb = [&](int x) -> uint64_t {
-          return x < L ? (uint64_t)b[x] : x == L ? (uint64_t)n0 : x == L + 1 ? (uint64_t)n1 : 0ull;
-        };
+    auto limb = [&](int x) -> uint64_t {
+      return x < L ? (uint64_t)b[x] : x == L ? (uint64_t)n0 : x == L + 1 ? (uint64_t)n1 : 0ull;
+    };
+    uint32_t u[NWM + 1];
 #pragma unroll
-        for (int k = k0; k < k1; ++k) {
-          const int bit = 32 * k - b0, jl = bit / W, sh = bit - jl * W;
-          const uint64_t v = limb(jl) | (limb(jl + 1) << W) | (limb(jl + 2) << (2 * W));
-          if (k < nwords) out[k] = (uint32_t)(v >> sh);
-        }
-      } else {
-        store_words_g<GG + 1>(b, n0, n1, out, nwords, g);
-      }
+    for (int i = 0; i <= NWM; ++i) {
+      const int bit = 32 * i, jl = bit / W, sh = bit - jl * W;
+      const uint64_t v = limb(jl) | (limb(jl + 1) << W) | (limb(jl + 2) << (2 * W));
+      u[i] = (uint32_t)(v >> sh);
+    }
+    const int b0 = G::g() * LB, ks = (b0 + 31) >> 5;
+    const int off = (ks << 5) - b0;  // [0, 32): local bit of the lane's first word
+    const int ke = (b0 + LB + 31) >> 5, kend = ke < nwords ? ke : nwords;
+    uint32_t* o = out + ks;
+#pragma unroll
+    for (int i = 0; i < NWM; ++i) {
+      const uint32_t w = (uint32_t)((((uint64_t)u[i + 1] << 32) | u[i]) >> off);
+      if (ks + i < kend) o[i] = w;
     }
   }
   // Store this lane's limbs one per word into an interleaved row.

@@ -695,11 +695,14 @@ struct WaveDig {
     const uint32_t hi = split3(cg, K + i) + (i == 0 ? e0 : 0u);
     const uint32_t hp = i == 0 ? 0u : split3(cg, K + i - 1) + (i == 1 ? e0 : 0u);
     if (!top) return (hi & MASK) + (hp >> W);
-    // positions 2K, 2K + 1 of U (column 2K is zero): split3(2K), split3(2K + 1)
+    // position 2K of U (column 2K is zero): split3(2K). (Position 2K + 1
+    // would weigh 2^(2W) in this limb: c' < 2^(W K + 2), so it is empty. A
+    // first form still added it as a 32-bit shift by 2W = 56 - undefined, and
+    // the compiler dropped the whole position-2K term with it: c' lost its
+    // bit W K whenever c' >= R, about one product in 4,000.)
     const uint64_t c1 = cg[2 * K - 1], c2 = cg[2 * K - 2];
     const uint32_t s2k = ((uint32_t)(c1 >> W) & MASK) + (uint32_t)(c2 >> (2 * W));
-    const uint32_t s2k1 = (uint32_t)(c1 >> (2 * W));
-    return hi + (hp >> W) + (s2k << W) + (s2k1 << (2 * W));
+    return hi + (hp >> W) + (s2k << W);
   }
 
   // (da, dc) = (pa, pc) (x) (ze, zf); zbw: the result also becomes the next

@@ -51,6 +51,10 @@ def available():
 # context's WIN_MARGIN table headroom) one new resident result may take;
 # larger batches stream through the host pipeline instead (xhe_*_host).
 RESIDENT_SHARE = 0.5
+# Batches up to this size skip the HBM query (torch's allocator statistics
+# cost ~0.1 ms per call, a visible share of a 64-element LR batch); the
+# context's WIN_MARGIN headroom covers them.
+RESIDENT_QUERY_MIN = 64 << 20
 
 
 def resident_budget(ctx, dev):
@@ -81,7 +85,8 @@ def device_for(ctx, num_cores=-1, count=0, elem_bytes=0):
     devs = ctx.shard_devices(num_cores)
     if len(devs) != 1:
         return None
-    if count and elem_bytes:
+    nbytes = count * elem_bytes
+    if nbytes and (nbytes > RESIDENT_QUERY_MIN or os.environ.get("XHE_RESIDENT_MAX_BYTES", "").strip()):
         cap = resident_budget(ctx, devs[0])
         if cap is not None and count * elem_bytes > cap:
             return None
