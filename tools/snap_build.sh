@@ -14,7 +14,7 @@ cp "$ROOT"/include/* "$SNAP/include/"
 (cd "$SNAP" && git -C "$ROOT" rev-parse --short HEAD > "$SNAP/HEAD" 2>/dev/null || true)
 {
   echo "snapshot $SNAP of $(cat "$SNAP/HEAD" 2>/dev/null)"
-  time /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -Rpass-analysis=kernel-resource-usage \
+  time /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Werror=shift-count-overflow -Werror=shift-count-negative "$@" -Rpass-analysis=kernel-resource-usage \
     -c "$SNAP/xfl_amd/csrc/xhe.hip" -o "$SNAP/xhe.o"
   g++ -O3 -std=c++17 -fPIC -pthread -c "$SNAP/xfl_amd/csrc/wire_abi.cpp" -o "$SNAP/wire_abi.o"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread "$SNAP/xhe.o" "$SNAP/wire_abi.o" -o "$OUT.tmp"

@@ -34,6 +34,11 @@ CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("XHE_OFFLOAD_ARCH", "gfx950")
 
 
+# warnings that mark undefined behaviour in the kernels are errors (a 32-bit
+# shift by 56 once silently dropped a term of WaveDig's top limb)
+WERROR = ["-Werror=shift-count-overflow", "-Werror=shift-count-negative"]
+
+
 def _stale(target, deps):
     if not os.path.exists(target):
         return True
@@ -65,7 +70,7 @@ def build(force=False, verbose=True, out=None, defines=()):
     dflags = [f"-D{d}" for d in defines]
     jobs = []
     if force or _stale(dev_obj, DEVICE_DEPS):
-        jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *dflags, "-c",
+        jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *WERROR, *dflags, "-c",
                      os.path.join(CSRC, "xhe.hip"), "-o", dev_obj + ".tmp"])
     if force or _stale(host_obj, HOST_DEPS):
         jobs.append([CXX, "-O3", "-std=c++17", "-fPIC", "-pthread", "-c", os.path.join(CSRC, "wire_abi.cpp"),

@@ -600,8 +600,60 @@ def _add(a, b):
     ca = ca._aligned_words(ops.n2w_of(ctx))
     ia, ib, shape = _bcast(ca, p)
     nout = int(np.prod(shape, dtype=np.int64))
-    enc = _encrypt_plain(ctx, _at(np.asarray(p).reshape(-1), ib) if p.ndim else np.repeat(np.asarray(p).reshape(1), nout))
+    P = _at(np.asarray(p).reshape(-1), ib) if p.ndim else np.repeat(np.asarray(p).reshape(1), nout)
+    enc = _plain_aligned(ctx, ca, ia, P)
+    if enc is None:
+        enc = _encrypt_plain(ctx, P)
     return _add_rows(ctx, ca, ia, enc, None, shape)
+
+
+def _plain_aligned(ctx, ca, ia, P):
+    """The scalar operand of ciphertext + scalar, encrypted and already at the
+    sum's exponent. The reference encrypts the scalar unobfuscated, c = 1 + n m
+    (paillier.py:95-101, 266-268), and where its exponent is the larger one
+    _decrease_exponent_to raises c to 2^d (paillier.py:79-86, 106-119). Since
+    (1 + n m)^(2^d) = 1 + n (m 2^d mod n) mod n^2 (the negative branch's
+    c^(2^d - n) as well), that is the plain encryption of m 2^d, the scalar
+    encoded at the ciphertext's exponent: a word shift on the host instead of
+    d squarings mod n^2 on the device. Device path only; None (encrypt, then
+    align, as before) off it, for scalars outside the vectorised encoder's
+    domain, or when m 2^d would come near n."""
+    dev = _res_dev(ctx, ca)
+    if dev is None or P.dtype == object:
+        return None
+    vec = _encode_scalars_vec(P)
+    if vec is None:
+        return None
+    kabs, neg, ep = (v.reshape(-1) for v in vec)
+    if kabs.size == 0:
+        return None
+    ec = ca._e.astype(np.int64)[ia] if ia is not None else ca._e.astype(np.int64).reshape(-1)
+    if ec.size != kabs.size:
+        ec = np.broadcast_to(ec, kabs.shape)
+    enew = np.minimum(ep, ec)
+    words, kbits = _shifted_words(kabs, ep - enew)
+    if kbits > ctx.n.bit_length() - 3:
+        return None
+    nw = ops.nw_of(ctx)
+    m = np.zeros((kabs.size, nw), np.uint32)
+    m[:, :words.shape[1]] = words
+    if neg.any():
+        m[neg] = _n_minus(ctx, m[neg], nw)
+    dk = ctx.device_key(dev)
+    ct = resident.encrypt_encoded(dk, m, False)
+    return PaillierArray.from_device(ctx, ct, enew.astype(np.int32), (kabs.size,))
+
+
+def _n_minus(ctx, x, nw):
+    """n - x for host words x [k, nw] (every x < n), vectorised borrow chain"""
+    nwd = nat.ints_to_words([ctx.n], nw)[0].astype(np.int64)
+    out = np.empty_like(x)
+    br = np.zeros(x.shape[0], np.int64)
+    for j in range(nw):
+        v = nwd[j] - x[:, j].astype(np.int64) - br
+        br = (v < 0).astype(np.int64)
+        out[:, j] = (v + (br << 32)).astype(np.uint32)
+    return out
 
 
 def _add_rows(ctx, ca, ia, cb, ib, shape):
