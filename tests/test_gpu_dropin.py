@@ -258,10 +258,11 @@ def test_larger_keys_tolerance_ops(fx):
 def test_add_plain_aligned_bit_exact(ctx_kind):
     """ciphertext + plaintext array on the device path, bit-exact against the
     reference's encrypt-then-align (paillier.py:95-123, oracle.add_scalar):
-    plaintexts whose exponent is above the ciphertext's (the scalar side is
-    encoded at the ciphertext's exponent, m 2^d, gaps up to ~1000 bits),
-    below it (the ciphertext is raised), equal, zero, negative, ints, and
-    Python-float scalars."""
+    plaintexts whose exponent is above the ciphertext's (the scalar encoded at
+    the ciphertext's exponent, m 2^d, gaps from 1 to ~1,000 bits), below it
+    (the ciphertext is raised), equal, zero, negative, ints and scalars; a
+    ciphertext at exponent -2076 takes the encrypt-then-align path (m 2^d past
+    n); |x| >= 2^53 raises as the reference's encoder does."""
     from oracle import paillier_oracle as O
     from xfl_amd.paillier import PaillierArray
     g = load_fixture("paillier_2048_djn.json")
@@ -269,17 +270,23 @@ def test_add_plain_aligned_bit_exact(ctx_kind):
     ctx = pub if ctx_kind == "pub" else priv
     ok = O.derive_private(priv.p, priv.q, priv.h_pow_n)
     rng = np.random.default_rng(3)
-    p = np.array([123.25, -7.5, 0.0, 1e-30, -3e-25, 1e300, -2.5e299, 335.0, -0.001, 2.0 ** 52, 1.0, -1.0])
-    # exponent -24 (precision 7) and -2076 (m 2^d past n: the encrypt-then-align path)
-    for base in (C.cts(ctx, g["encrypt"]["priv_f32_p7"])[:1], C.cts(ctx, g["ops"]["gap_operands"])[:1]):
-        A = PaillierArray(np.array([base[0]] * 12, dtype=object))
-        A.to_device()
-        p32 = np.array([123.25, -7.5, 0.0, 1e-30, -3e-25, 3e38, -2.5e37, 335.0, -0.001, 2.0 ** 52, 1.0, -1.0], np.float32)
+    p = np.array([123.25, -7.5, 0.0, 1e-30, -3e-25, 2.0 ** 52 + 1, -4.5e15, 335.0, -0.001, 2.0 ** -600, 1.0, -1.0])
+    p32 = p.astype(np.float32)
+    base = C.cts(ctx, g["encrypt"]["priv_f32_p7"])[:1]  # exponent -24
+    A0 = PaillierArray(np.array([base[0]] * 12, dtype=object))
+    A0.to_device()
+    deep = A0 * (2.0 ** -900)  # exponent -976: gaps of ~930 bits
+    far = PaillierArray(np.array(C.cts(ctx, g["ops"]["gap_operands"])[:1].tolist() * 12, dtype=object))
+    far.to_device()  # exponent -2076
+    for A in (A0, deep, far):
+        raws, exps = C.raw(A)
         for P in (p, p32, rng.integers(-1000, 1000, 12).astype(np.int64)):
             got = A + P
-            want = [O.add_scalar(ok, base[0].raw_ciphertext, base[0].exponent, v.item()) for v in P]
+            want = [O.add_scalar(ok, r, e, v.item()) for r, e, v in zip(raws, exps, P)]
             assert C.raw(got) == ([w[0] for w in want], [w[1] for w in want])
-        for s in (3.75, -1e200, 7):
-            got = A + s
-            want = O.add_scalar(ok, base[0].raw_ciphertext, base[0].exponent, s)
-            assert C.raw(got) == ([want[0]] * 12, [want[1]] * 12)
+        for sc in (3.75, -2.5e-9, 7):
+            got = A + sc
+            want = [O.add_scalar(ok, r, e, sc) for r, e in zip(raws, exps)]
+            assert C.raw(got) == ([w[0] for w in want], [w[1] for w in want])
+        with pytest.raises(ValueError):
+            A + np.full(12, 1e300)

@@ -75,6 +75,7 @@ template <int K, int NWV, int W_ = 28>
 struct WaveMont {
   static constexpr int W = W_;  // 28 mod P^2 (k_dec_wave); 27 mod n^2 (k_mexp_horner_wave: 2K W-bit
                                 // products per column stay below 2^64 at K = 154)
+  static constexpr int K_ = K;
   static constexpr uint32_t MASK = (1u << W) - 1u;
   static constexpr int NT = 64 * NWV;  // threads per residue
   // terms per slice: 8 when the threads hold every (quad, 8-term slice), else 16
@@ -600,6 +601,152 @@ __global__ void __launch_bounds__(64 * NWV) k_mulmod_wave(KeyDev key, const uint
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Batch inversion mod n^2 for small batches (2048-bit keys, up to 256
+// elements: the LR step's bases with negative coefficients) as a product
+// tree of whole-block WaveMont products, one block per node and one launch
+// per level: the tree's latency is its depth in products (~5 us each), not
+// the 16-lane shape's ~25 us per product (k_tree_up_block/_down_block).
+// Nodes are kept in wave-limb form (K limbs of 27 bits) times R_w; the root
+// leaves in plain words for the host's inverse and comes back the same way.
+template <class WM>
+XHE_DEV void wave_init_n2(typename WM::Lds& s, const KeyDev& key) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+  for (int i = WM::tid(); i < (int)(sizeof(s) / 4); i += WM::NT) w[i] = 0u;
+  WM::sync();
+  for (int i = WM::tid(); i < WM::K_; i += WM::NT) {
+    s.zn[WM::ZO + i] = key.n2w_N[i];
+    s.znp[WM::ZO + i] = key.n2w_np[i];
+  }
+}
+// limbs of a packed residue (nwords words)
+template <class WM>
+XHE_DEV void wave_limbs_in(const uint32_t* __restrict__ wv, int nwords, uint32_t* dst) {
+  for (int i = WM::tid(); i < WM::K_; i += WM::NT) {
+    const int bit = WM::W * i, k = bit >> 5, sh = bit & 31;
+    const uint32_t lo = k < nwords ? wv[k] : 0u, hi = k + 1 < nwords ? wv[k + 1] : 0u;
+    dst[i] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & WM::MASK;
+  }
+}
+// x (< 2N, limbs <= MASK + 2) -> x mod N packed into nwords words, by thread 0
+template <class WM>
+XHE_DEV void wave_words_out(uint32_t* x, const uint32_t* zn, int nwords, uint32_t* __restrict__ o) {
+  constexpr int K = WM::K_;
+  if (WM::tid() != 0) return;
+  uint32_t cy = 0;
+  for (int i = 0; i < K; ++i) {
+    const uint32_t t = x[i] + cy;
+    x[i] = t & WM::MASK;
+    cy = t >> WM::W;
+  }
+  int64_t br = 0;
+  for (int i = 0; i < K; ++i) br = ((int64_t)x[i] - (int64_t)zn[WM::ZO + i] + br) >> WM::W;
+  if (br == 0) {  // x >= N
+    for (int i = 0; i < K; ++i) {
+      const int64_t t = (int64_t)x[i] - (int64_t)zn[WM::ZO + i] + br;
+      x[i] = (uint32_t)t & WM::MASK;
+      br = t >> WM::W;
+    }
+  }
+  uint64_t acc = 0;
+  int have = 0, wi = 0;
+  for (int i = 0; i < K && wi < nwords; ++i) {
+    acc |= (uint64_t)x[i] << have;
+    have += WM::W;
+    while (have >= 32 && wi < nwords) {
+      o[wi++] = (uint32_t)acc;
+      acc >>= 32;
+      have -= 32;
+    }
+  }
+  while (wi < nwords) {
+    o[wi++] = (uint32_t)acc;
+    acc >>= 32;
+  }
+}
+
+// mode 0: node[e] = words[e] R_w (MontW(x, R_w^2)); mode 1: root words
+// (plain inverse from the host) -> inv node, the same conversion
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_wtree_in(KeyDev key, const uint32_t* __restrict__ words,
+                                                       uint32_t* __restrict__ node) {
+  using WM = WaveMont<K, NWV, 27>;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int64_t e = blockIdx.x;
+  wave_init_n2<WM>(s, key);
+  wave_limbs_in<WM>(words + (size_t)e * key.n2w, key.n2w, s.tl);
+  for (int i = WM::tid(); i < K; i += WM::NT) s.zb[WM::ZO + i] = key.n2w_R2[i];
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, false);
+  for (int i = WM::tid(); i < K; i += WM::NT) node[(size_t)e * K + i] = s.x[i];
+}
+
+// up-sweep level: parent i = child 2i x child 2i+1 (a lone last child is
+// copied up)
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_wtree_up(KeyDev key, const uint32_t* __restrict__ child, int64_t nchild,
+                                                       uint32_t* __restrict__ parent) {
+  using WM = WaveMont<K, NWV, 27>;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int64_t i = blockIdx.x;
+  const uint32_t* a = child + (size_t)(2 * i) * K;
+  if (2 * i + 1 >= nchild) {
+    for (int j = WM::tid(); j < K; j += WM::NT) parent[(size_t)i * K + j] = a[j];
+    return;
+  }
+  wave_init_n2<WM>(s, key);
+  for (int j = WM::tid(); j < K; j += WM::NT) {
+    s.tl[j] = a[j];
+    s.zb[WM::ZO + j] = a[K + j];
+  }
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, false);
+  for (int j = WM::tid(); j < K; j += WM::NT) parent[(size_t)i * K + j] = s.x[j];
+}
+
+// down-sweep level: inv child i = inv parent (i/2) x node sibling (i^1), or
+// the parent's inverse for a lone child
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_wtree_down(KeyDev key, const uint32_t* __restrict__ inv_parent,
+                                                         const uint32_t* __restrict__ node, int64_t nchild,
+                                                         uint32_t* __restrict__ inv_child) {
+  using WM = WaveMont<K, NWV, 27>;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int64_t i = blockIdx.x, sib = i ^ 1;
+  const uint32_t* ip = inv_parent + (size_t)(i >> 1) * K;
+  if (sib >= nchild) {
+    for (int j = WM::tid(); j < K; j += WM::NT) inv_child[(size_t)i * K + j] = ip[j];
+    return;
+  }
+  wave_init_n2<WM>(s, key);
+  for (int j = WM::tid(); j < K; j += WM::NT) {
+    s.tl[j] = ip[j];
+    s.zb[WM::ZO + j] = node[(size_t)sib * K + j];
+  }
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, false);
+  for (int j = WM::tid(); j < K; j += WM::NT) inv_child[(size_t)i * K + j] = s.x[j];
+}
+
+// node[e] R_w -> plain words (MontW(x R_w, 1), reduced below N)
+template <int K, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_wtree_out(KeyDev key, const uint32_t* __restrict__ node,
+                                                        uint32_t* __restrict__ words) {
+  using WM = WaveMont<K, NWV, 27>;
+  __shared__ __attribute__((aligned(16))) typename WM::Lds s;
+  const int64_t e = blockIdx.x;
+  wave_init_n2<WM>(s, key);
+  for (int j = WM::tid(); j < K; j += WM::NT) s.tl[j] = node[(size_t)e * K + j];
+  if (WM::tid() == 0) s.zb[WM::ZO] = 1u;
+  WM::sync();
+  int cur = 0;
+  WM::mul(s, cur, s.tl, s.x, false);
+  wave_words_out<WM>(s.x, s.zn, key.n2w, words + (size_t)e * key.n2w);
+}
 
 // ---------------------------------------------------------------------------
 // Montgomery DIGITS mod P^2 (pdigit_dev.hpp's PMD: x R^2 = R a + P c mod P^2,

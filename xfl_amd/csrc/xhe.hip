@@ -1248,15 +1248,26 @@ bool n2_row(int64_t count) {
   return pin ? pin == 16 : count <= kN2RowMax;
 }
 
-// Aligned adds of a few elements with long alignment chains run one 16-wave
-// block per element (k_mulmod_wave, 2048-bit keys): up to kWaveAddMax
-// elements when the largest gap is at least kWaveAddMinD squarings.
-// $XHE_ADD_WAVE=0 keeps the lane shapes (A/B).
+// Adds of a few elements run one 16-wave block per element (k_mulmod_wave,
+// 2048-bit keys) up to kWaveAddMax elements, with or without alignment
+// squarings (kWaveAddMinD: the plain product of the LR step's noise add, 15
+// elements, took 56 us in the 16-lane k_mulmod_n2). $XHE_ADD_WAVE=0 keeps
+// the lane shapes (A/B).
 constexpr int64_t kWaveAddMax = 256;
-constexpr int kWaveAddMinD = 4;
+constexpr int kWaveAddMinD = 0;
 bool add_wave_on() {
   static const bool on = [] {
     const char* e = getenv("XHE_ADD_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Small-batch inversion as a tree of whole-block products (k_wtree_*);
+// $XHE_TREE_WAVE=0 keeps the single-block 16-lane sweeps (A/B).
+bool tree_wave_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_TREE_WAVE");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1340,6 +1351,56 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
     tot += (size_t)S4 * n;
   }
   if constexpr (Sh::K == 2048 && MN2::TPI == 16) {  // (a 1024-thread block: the 16-lane 2048-bit shape's registers)
+  if (count <= 256 && tree_wave_on()) {
+    // small batch: a product tree of whole-block products (dec_wave.hpp
+    // k_wtree_*), one launch per level
+    constexpr int KW = 154;
+    std::vector<int64_t> woff;
+    int64_t wtot = 0;
+    for (auto n : sizes) {
+      woff.push_back(wtot);
+      wtot += n;
+    }
+    const int nlev = (int)sizes.size();
+    uint32_t *lv = nullptr, *inv = nullptr, *wds = nullptr;
+    HIPCHK(hipMallocAsync((void**)&lv, (size_t)wtot * KW * 4, s));
+    HIPCHK(hipMallocAsync((void**)&inv, (size_t)wtot * KW * 4, s));
+    HIPCHK(hipMallocAsync((void**)&wds, (size_t)2 * k->n2w * 4, s));
+    auto node = [&](uint32_t* b, int l) { return b + (size_t)woff[l] * KW; };
+    hipLaunchKernelGGL((k_wtree_in<KW, 16>), dim3((unsigned)count), dim3(1024), 0, s, k->kd, c, lv);
+    HIPCHK(hipGetLastError());
+    for (int l = 1; l < nlev; ++l) {
+      hipLaunchKernelGGL((k_wtree_up<KW, 16>), dim3((unsigned)sizes[l]), dim3(1024), 0, s, k->kd, node(lv, l - 1),
+                         sizes[l - 1], node(lv, l));
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_wtree_out<KW, 16>), dim3(1), dim3(1024), 0, s, k->kd, node(lv, nlev - 1), wds);
+    HIPCHK(hipGetLastError());
+    std::vector<uint32_t> root(k->n2w), yinv(k->n2w);
+    HIPCHK(hipMemcpyAsync(root.data(), wds, (size_t)k->n2w * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!modinv_words(root.data(), k->n2_host.data(), k->n2w, yinv.data())) {
+      (void)hipFreeAsync(lv, s);
+      (void)hipFreeAsync(inv, s);
+      (void)hipFreeAsync(wds, s);
+      return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
+    }
+    HIPCHK(hipMemcpyAsync(wds + k->n2w, yinv.data(), (size_t)k->n2w * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL((k_wtree_in<KW, 16>), dim3(1), dim3(1024), 0, s, k->kd, wds + k->n2w, node(inv, nlev - 1));
+    HIPCHK(hipGetLastError());
+    for (int l = nlev - 2; l >= 0; --l) {
+      hipLaunchKernelGGL((k_wtree_down<KW, 16>), dim3((unsigned)sizes[l]), dim3(1024), 0, s, k->kd, node(inv, l + 1),
+                         node(lv, l), sizes[l], node(inv, l));
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_wtree_out<KW, 16>), dim3((unsigned)count), dim3(1024), 0, s, k->kd, inv, out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // yinv is host memory of this frame
+    (void)hipFreeAsync(lv, s);
+    (void)hipFreeAsync(inv, s);
+    (void)hipFreeAsync(wds, s);
+    return XHE_OK;
+  }
   if (count <= 256) {
     // small batch: one block per sweep (k_tree_up_block / k_tree_down_block)
     const int nlev = (int)sizes.size();

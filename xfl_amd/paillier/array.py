@@ -645,7 +645,11 @@ def _plain_aligned(ctx, ca, ia, P):
 
 
 def _n_minus(ctx, x, nw):
-    """n - x for host words x [k, nw] (every x < n), vectorised borrow chain"""
+    """n - x for host words x [k, nw] (every x < n): Python ints for small
+    batches, else a borrow chain vectorised over the rows"""
+    if x.shape[0] <= 1024:
+        n = ctx.n
+        return nat.ints_to_words([n - v for v in nat.words_to_ints(x)], nw)
     nwd = nat.ints_to_words([ctx.n], nw)[0].astype(np.int64)
     out = np.empty_like(x)
     br = np.zeros(x.shape[0], np.int64)
