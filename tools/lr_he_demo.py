@@ -79,7 +79,13 @@ def expected_noised_gradient(okey, resid32, x32, noise32):
     return np.array(out, dtype=np.float32)
 
 
-def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
+def _sync():
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, sync_phases=False):
     """Runs the HE rounds; returns a dict of phase timings and check results."""
     from xfl_amd.paillier import Paillier, PaillierContext
     xtr, ytr, _, _ = load_wdbc()
@@ -117,6 +123,8 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
             resid = (yb - pred).astype(np.float32)  # label side
             a = time.time()
             enc = Paillier.encrypt(priv, resid.astype(np.float32).flatten(), precision=7, obfuscation=True)
+            if sync_phases:
+                _sync()
             tm["encrypt"] += time.time() - a
             a = time.time()
             wire = Paillier.serialize(enc)
@@ -127,9 +135,13 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0):
             noise /= 100000
             a = time.time()
             g = np.matmul(enc_t, xb_t)
+            if sync_phases:
+                _sync()
             tm["matmul"] += time.time() - a
             a = time.time()
             g = g + noise
+            if sync_phases:
+                _sync()
             tm["add_noise"] += time.time() - a
             a = time.time()
             wire2 = Paillier.serialize(g)
@@ -199,9 +211,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--sync-phases", action="store_true",
+                    help="synchronise the device at the end of every phase (per-phase latency, diagnostic)")
     ap.add_argument("--cpu-batches", type=int, default=1, help="batches timed through the CPU restatement (0: skip)")
     args = ap.parse_args()
-    rec = run(epochs=args.epochs, check=args.check)
+    rec = run(epochs=args.epochs, check=args.check, sync_phases=args.sync_phases)
     if args.cpu_batches:
         rec["cpu_restatement_s_per_batch"] = sum(cpu_batch_seconds(seed=i) for i in range(args.cpu_batches)) / \
             args.cpu_batches
