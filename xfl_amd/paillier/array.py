@@ -639,8 +639,13 @@ def _plain_aligned(ctx, ca, ia, P):
     m[:, :words.shape[1]] = words
     if neg.any():
         m[neg] = _n_minus(ctx, m[neg], nw)
-    dk = ctx.device_key(dev)
-    ct = resident.encrypt_encoded(dk, m, False)
+    if kabs.size <= 1024:
+        # 1 + n m (< n^2, paillier.py:266-268) on the host: cheaper than a
+        # launch of the one-lane k_raw_enc for the LR step's 15 elements
+        n = ctx.n
+        ct = resident.upload(nat.ints_to_words([1 + n * v for v in nat.words_to_ints(m)], 2 * nw), dev)
+    else:
+        ct = resident.encrypt_encoded(ctx.device_key(dev), m, False)
     return PaillierArray.from_device(ctx, ct, enew.astype(np.int32), (kabs.size,))
 
 
