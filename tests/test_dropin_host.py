@@ -199,3 +199,32 @@ def test_shifted_words_matches_python_ints():
         assert words_to_ints(w) == want
         assert max(v.bit_length() for v in want) <= kbits
 
+
+
+def test_encode_at_aligned_exponent_matches_encoder():
+    """array._encode_at (the host half of ciphertext + scalar's aligned
+    operand): each scalar's encoding at min(its own exponent, the
+    ciphertext's) is the reference's encode_single at its own exponent times
+    2^d mod n - the plaintext of (1 + n m)^(2^d), what _decrease_exponent_to
+    makes of the encrypted scalar (paillier.py:79-86) - for floats of both
+    signs, zero, float32, ints and gaps up to ~1,100 bits; None when a value
+    would come near n."""
+    import numpy as np
+    from oracle import paillier_oracle as O
+    from xfl_amd._native import words_to_ints
+    from tests.conftest import load_fixture
+    from xfl_amd.paillier.array import _encode_at
+    g = load_fixture("paillier_2048_djn.json")
+    priv, _ = C.ctxs(g)
+    ok = O.derive_private(priv.p, priv.q, priv.h_pow_n)
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.standard_normal(20) * 10.0 ** rng.integers(-30, 12, 20), [0.0, -1.0, 2.0 ** 52]])
+    cases = ((x, rng.integers(-1100, 10, x.size)), (x.astype(np.float32), np.full(x.size, -40)),
+             (rng.integers(-10 ** 6, 10 ** 6, 9), rng.integers(-900, 5, 9)))
+    for P, ec in cases:
+        m, enew = _encode_at(priv, P, ec)
+        for v, c, e, got in zip(P.tolist(), ec.tolist(), enew.tolist(), words_to_ints(m)):
+            ep = 0 if isinstance(v, int) else O.cal_exponent_float(v, None)
+            assert e == min(ep, c)
+            assert got == (O.encode(ok, v, ep) << (ep - e)) % priv.n, (v, ep, e)
+    assert _encode_at(priv, np.array([3.0]), np.array([-2100])) is None

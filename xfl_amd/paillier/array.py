@@ -619,7 +619,30 @@ def _plain_aligned(ctx, ca, ia, P):
     align, as before) off it, for scalars outside the vectorised encoder's
     domain, or when m 2^d would come near n."""
     dev = _res_dev(ctx, ca)
-    if dev is None or P.dtype == object:
+    if dev is None:
+        return None
+    ec = ca._e.astype(np.int64)[ia] if ia is not None else ca._e.astype(np.int64).reshape(-1)
+    enc = _encode_at(ctx, P, ec)
+    if enc is None:
+        return None
+    m, enew = enc
+    k, nw = m.shape
+    if k <= 1024:
+        # 1 + n m (< n^2, paillier.py:266-268) on the host: cheaper than a
+        # launch of the one-lane k_raw_enc for the LR step's 15 elements
+        n = ctx.n
+        ct = resident.upload(nat.ints_to_words([1 + n * v for v in nat.words_to_ints(m)], 2 * nw), dev)
+    else:
+        ct = resident.encrypt_encoded(ctx.device_key(dev), m, False)
+    return PaillierArray.from_device(ctx, ct, enew.astype(np.int32), (k,))
+
+
+def _encode_at(ctx, P, ec):
+    """encode_single of every scalar of P at exponent min(its own, ec)
+    (encoder.py:48-54 at the aligned exponent, < n/8): (m words [k, nw],
+    exponents), or None outside the vectorised encoder's domain or when a
+    value would come near n"""
+    if P.dtype == object:
         return None
     vec = _encode_scalars_vec(P)
     if vec is None:
@@ -627,9 +650,7 @@ def _plain_aligned(ctx, ca, ia, P):
     kabs, neg, ep = (v.reshape(-1) for v in vec)
     if kabs.size == 0:
         return None
-    ec = ca._e.astype(np.int64)[ia] if ia is not None else ca._e.astype(np.int64).reshape(-1)
-    if ec.size != kabs.size:
-        ec = np.broadcast_to(ec, kabs.shape)
+    ec = np.broadcast_to(np.asarray(ec, dtype=np.int64).reshape(-1), kabs.shape)
     enew = np.minimum(ep, ec)
     words, kbits = _shifted_words(kabs, ep - enew)
     if kbits > ctx.n.bit_length() - 3:
@@ -639,14 +660,7 @@ def _plain_aligned(ctx, ca, ia, P):
     m[:, :words.shape[1]] = words
     if neg.any():
         m[neg] = _n_minus(ctx, m[neg], nw)
-    if kabs.size <= 1024:
-        # 1 + n m (< n^2, paillier.py:266-268) on the host: cheaper than a
-        # launch of the one-lane k_raw_enc for the LR step's 15 elements
-        n = ctx.n
-        ct = resident.upload(nat.ints_to_words([1 + n * v for v in nat.words_to_ints(m)], 2 * nw), dev)
-    else:
-        ct = resident.encrypt_encoded(ctx.device_key(dev), m, False)
-    return PaillierArray.from_device(ctx, ct, enew.astype(np.int32), (kabs.size,))
+    return m, enew
 
 
 def _n_minus(ctx, x, nw):
