@@ -627,9 +627,10 @@ def _plain_aligned(ctx, ca, ia, P):
         return None
     m, enew = enc
     k, nw = m.shape
-    if k <= 1024:
-        # 1 + n m (< n^2, paillier.py:266-268) on the host: cheaper than a
-        # launch of the one-lane k_raw_enc for the LR step's 15 elements
+    if k <= 64:
+        # 1 + n m (< n^2, paillier.py:266-268) on the host (~5 us an element,
+        # overlapping the device's queue): for the LR step's 15 elements
+        # cheaper than the one-lane k_raw_enc launch behind it (~85 us)
         n = ctx.n
         ct = resident.upload(nat.ints_to_words([1 + n * v for v in nat.words_to_ints(m)], 2 * nw), dev)
     else:
@@ -666,7 +667,7 @@ def _encode_at(ctx, P, ec):
 def _n_minus(ctx, x, nw):
     """n - x for host words x [k, nw] (every x < n): Python ints for small
     batches, else a borrow chain vectorised over the rows"""
-    if x.shape[0] <= 1024:
+    if x.shape[0] <= 256:
         n = ctx.n
         return nat.ints_to_words([n - v for v in nat.words_to_ints(x)], nw)
     nwd = nat.ints_to_words([ctx.n], nw)[0].astype(np.int64)
