@@ -131,9 +131,9 @@ def pmc_traffic(win_bits, n, kernel="k_djn_pmd"):
         if rec.get("kernel", kernel) != kernel and rnd == "r4":
             continue
         if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
-            return None, None
-        return rec["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+            return None, None, None
+        return rec["traffic_bytes"], os.path.relpath(path, ROOT), rec
+    return None, None, None
 
 
 def _timed(fn, reps=3):
@@ -558,7 +558,7 @@ def main():
         w_elem, w_pow = algorithmic_macs_per_element(bits, args.win, dk.rand_bits)
         pow_avg_s = (tot.value / max(cnt.value, 1)) / 1e3
         achieved = N * w_pow / pow_avg_s / 1e12  # N elements x 2 primes per launch
-        traffic, traffic_src = pmc_traffic(args.win, N, kname) if bits == 2048 else (None, None)
+        traffic, traffic_src, pmc = pmc_traffic(args.win, N, kname) if bits == 2048 else (None, None, None)
         rec = {
             "metric": "2048-bit Paillier encrypts/s (device-resident)" if bits == 2048 else f"{bits}-bit Paillier encrypts/s (device-resident)",
             "value": value, "unit": "encrypts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -577,6 +577,11 @@ def main():
             "parity_sample_ok": parity_ok,
             "key_setup_s": t_key,
         }
+        if pmc and pmc.get("clock_ghz"):
+            # the counter pass's clock under this load (SQ_BUSY_CYCLES) and VALU
+            # busy: `peak` is the 2.4 GHz figure, the kernel runs below it
+            rec["roofline"].update({"pmc_clock_ghz": float(pmc["clock_ghz"]),
+                                    "pmc_valu_busy_frac": pmc.get("valu_busy_frac")})
         rec["config"]["table_bytes"] = nat.table_bytes(bits, args.win)
         if not args.no_ops and (args.win & 0xFF) != 16:
             rec["headline_dropin_window"] = headline_at_window(nat, L, bits, (p, q, n, h), 16, x, m, ex, st, rnd, N,
