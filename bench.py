@@ -121,14 +121,16 @@ def pmc_traffic(win_bits, n, kernel="k_djn_pmd"):
     kernel changed between rounds; before round 4 the files were named after
     the k_djn_pow label)."""
     from xfl_amd._native import win_spec
-    for rnd, name in (("r4", kernel), ("r3", "k_djn_pow"), ("r2", "k_djn_pow")):
+    for rnd, name in (("r5", kernel), ("r4", kernel), ("r3", "k_djn_pow"), ("r2", "k_djn_pow")):
+        if name != kernel:  # an older round's pass measured another kernel: not this one's traffic
+            continue
         path = os.path.join(ROOT, "profiles", rnd, f"{name}_pmc.json")
         try:
             with open(path) as f:
                 rec = json.load(f)
         except (OSError, ValueError):
             continue
-        if rec.get("kernel", kernel) != kernel and rnd == "r4":
+        if rec.get("kernel", kernel) != kernel:
             continue
         if str(rec.get("win")) != win_spec(win_bits) or rec.get("n") != n or "traffic_bytes" not in rec:
             return None, None, None
@@ -343,6 +345,11 @@ def measure_dropin(nat, device, key_bits, xh, key_material):
     ctx._volume = ctx.WIN_STEPS[-1][0]
     out["dropin_encrypt_steady_per_s"] = nh / _timed(enc_only, reps=3)
     win["dropin_encrypt_steady_per_s"] = ctx._dev[device].win_bits
+    # the steady window's ciphertexts decrypt back to the inputs (to the
+    # precision-7 encoding and the float32 result)
+    back = Paillier.decrypt(ctx, enc[0])
+    out["dropin_encrypt_steady_max_abs_err"] = float(np.max(np.abs(back - x32)))
+    out["dropin_encrypt_steady_ok"] = bool(np.allclose(back, x32, rtol=1e-6, atol=1e-7))
     out["dropin_table_bytes_steady"] = nat.table_bytes(key_bits, ctx._dev[device].win_bits)
     out["dropin_window_bits"] = win
     wire.clear()
@@ -450,6 +457,10 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group and gather through it even at --gpus 1 (the N-GPU "
                          "code path - init, async all-gather, barriers, max-over-ranks all-reduce - on one GPU)")
+    ap.add_argument("--proxy-world", type=int, default=0,
+                    help="with --dist: size the gather target for this many ranks and move the other ranks' share of "
+                         "the vector every step too (a one-GPU stand-in for the P-rank job's gather bytes and memory; "
+                         "shard.GatherPipeline proxy_world)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -504,24 +515,37 @@ def main():
         nat.check(L.xhe_rand(dk.handle, seed32, i, N, rnd.data_ptr(), None, stream), "rand")
         nat.check(L.xhe_encrypt(dk.handle, m.data_ptr(), rnd.data_ptr(), N, ct.data_ptr(), stream), "encrypt")
 
-    pipe = GatherPipeline(encrypt_shard, N, dk.n2w, world=world, rank=rank, device="cuda", collective=use_dist)
+    pipe = GatherPipeline(encrypt_shard, N, dk.n2w, world=world, rank=rank, device="cuda", collective=use_dist,
+                          proxy_world=args.proxy_world or None)
     last = 1_000_000 + max(args.warmup, 1) - 1  # the parity check below needs one finished step
     for i in range(1_000_000, last + 1):
         pipe.step(i)
     pipe.drain()
     torch.cuda.synchronize()
-    # parity spot check of this rank's output against the oracle (not timed)
+    # parity check of this rank's output (not timed): 4,096 elements spread
+    # over the shard against the reference's encryption on the same draws -
+    # the oracle's encode (encoder.py:29-54) and the GMP port's DJN-CRT
+    # encryption (oracle/gmp_baseline.c, pinned to the golden ciphertexts);
+    # the pure-Python oracle on 4 of them when libgmp is not loadable
+    from oracle import bench_cpu
     from oracle import paillier_oracle as O
     okey = O.derive_private(p, q, h)
-    idx = [0, 1, N // 2, N - 1]
     xs = x.cpu().numpy()
     rnd_h = rnd.cpu().numpy().view(np.uint32)
+    idx = np.unique(np.concatenate([[0, 1, N // 2, N - 1], np.random.default_rng(7).integers(0, N, 4092)]))
+    ms = [O.encode_element(okey, float(xs[i]), 7)[0] for i in idx]
+    try:
+        want = bench_cpu.gmp_encrypt_batch(okey, nat.ints_to_words(ms, dk.nw), rnd_h[idx], threads=host_cores()[0])
+        want = dict(zip(idx.tolist(), nat.words_to_ints(want)))
+    except RuntimeError:
+        idx = idx[[0, 1, -2, -1]]
+        want = {int(i): O.encrypt_m(okey, O.encode_element(okey, float(xs[i]), 7)[0], nat.words_to_ints(rnd_h[i]))
+                for i in idx}
+    parity_n = len(idx)
+    parity_ok = shard_parity(pipe.shard(last), pipe.vector(last) if use_dist else None, rank, [int(i) for i in idx],
+                             want.__getitem__)
 
-    def expected(i):
-        return O.encrypt_m(okey, O.encode_element(okey, float(xs[i]), 7)[0], nat.words_to_ints(rnd_h[i]))
-
-    parity_ok = shard_parity(pipe.shard(last), pipe.vector(last) if use_dist else None, rank, idx, expected)
-
+    free_after = int(torch.cuda.mem_get_info(local)[0])
     L.xhe_profile(1)
     if use_dist:
         dist.barrier()
@@ -575,8 +599,14 @@ def main():
                          "alg_macs_per_element": w_pow,
                          "alg_table_bytes_per_launch": N * 2 * nat.win_layout(dk.rand_bits, args.win)[0] * TABLE_ROW_BYTES[bits]},
             "parity_sample_ok": parity_ok,
+            "parity_sample_n": parity_n,
             "key_setup_s": t_key,
+            "hbm_free_after_setup_bytes": free_after,
         }
+        if pipe.proxy:
+            rec["config"]["proxy_world"] = pipe.proxy
+            rec["config"]["proxy_gather_bytes_per_step"] = (pipe.proxy - world) * N * dk.n2w * 4
+            rec["config"]["gather_target_bytes"] = sum(g.numel() * 4 for g in pipe.gathered)
         if pmc and pmc.get("clock_ghz"):
             # the counter pass's clock under this load (SQ_BUSY_CYCLES) and VALU
             # busy: `peak` is the 2.4 GHz figure, the kernel runs below it

@@ -75,6 +75,31 @@ def gmp_encrypt_one(k, m, a):
     return int.from_bytes(out.tobytes(), "little")
 
 
+def gmp_encrypt_batch(k, m_words, a_words, threads=8):
+    """DJN-CRT private encryptions (1 + n m) h^a mod n^2 of encoded residues
+    through the GMP port, many threads: the checker of the GPU parity tests at
+    sizes the pure-Python oracle cannot finish in seconds. m_words [count][nw],
+    a_words [count][aw] little-endian uint32; returns [count][2 nw] uint32."""
+    import ctypes
+    import numpy as np
+    L = _gmp_lib()
+    if L is None:
+        raise RuntimeError("libgmp.so.10 not loadable: GMP checker unavailable")
+    nw = (k["n"].bit_length() + 31) // 32
+    m_words = np.ascontiguousarray(m_words, dtype=np.uint32)
+    a_words = np.ascontiguousarray(a_words, dtype=np.uint32)
+    count, aw = a_words.shape
+    assert m_words.shape == (count, nw), (m_words.shape, count, nw)
+    arrs = _key_words(k, nw)
+    out = np.zeros((count, 2 * nw), dtype=np.uint32)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    rc = L.gmpb_encrypt_batch(*[vp(x) for x in arrs], ctypes.c_int(nw), vp(m_words), vp(a_words), ctypes.c_int(aw),
+                              ctypes.c_int64(count), ctypes.c_int(threads), vp(out))
+    if rc != 0:
+        raise RuntimeError(f"gmpb_encrypt_batch failed: {rc}")
+    return out
+
+
 def gmp_rate(bits, seconds, threads):
     """(encryptions, wall seconds) of the GMP port over `threads` threads, or None."""
     import ctypes

@@ -6,7 +6,10 @@
  * on the same GMP routines gmpy2 calls (mpz_powm / mpz_mul / mpz_fdiv_r),
  * loaded from the system libgmp.so.10 with dlopen (no GMP headers in the
  * image, so the few prototypes used are declared here; mpz_t layout is GMP's
- * stable public ABI). Used as bench.py's cpu_baseline when it builds/loads.
+ * stable public ABI). Used as bench.py's cpu_baseline when it builds/loads,
+ * and (gmpb_encrypt_batch) as the fast checker of the GPU parity tests at the
+ * production table windows, after tests/test_cpu_baseline.py has pinned it to
+ * the reference's golden ciphertexts.
  */
 #include <dlfcn.h>
 #include <math.h>
@@ -119,6 +122,69 @@ int gmpb_encrypt_one(const uint32_t* n, const uint32_t* n2, const uint32_t* p2, 
   size_t cnt = 0;
   z_export(out_words, &cnt, -1, 4, 0, 0, out);
   z_clear(out); z_clear(t1); z_clear(t2); z_clear(a); z_clear(mm);
+  key_clear(&k);
+  return 0;
+}
+
+/* Batch checker for the GPU parity tests: c_i = (1 + n m_i) * CRT(hp^a_i mod p^2,
+ * hq^a_i mod q^2) mod n^2 (paillier.py:189-209,283; utils.py:38-43) for full
+ * nw-word residues m_i (already encoded, 0 <= m_i < n) and aw-word a_i, on
+ * `threads` threads. Elements i = t, t + threads, ... go to thread t. */
+typedef struct {
+  const key_t_* k;
+  const uint32_t* m;
+  const uint32_t* a;
+  uint32_t* out;
+  int64_t count;
+  int aw, t, threads;
+} batch_t;
+
+static void* batch_worker(void* arg) {
+  batch_t* b = (batch_t*)arg;
+  const key_t_* k = b->k;
+  const int nw = k->nw;
+  mpz_t out, t1, t2, a, m;
+  z_init(out); z_init(t1); z_init(t2); z_init(a); z_init(m);
+  for (int64_t i = b->t; i < b->count; i += b->threads) {
+    imp(m, b->m + (size_t)i * nw, nw);
+    z_import(a, (size_t)b->aw, -1, 4, 0, 0, b->a + (size_t)i * b->aw);
+    z_mul(t1, k->n, m);
+    z_add_ui(t1, t1, 1);
+    z_fdiv_r(out, t1, k->n2);
+    z_powm(t1, k->hp, a, k->p2);
+    z_powm(t2, k->hq, a, k->q2);
+    z_sub(m, t1, t2);
+    z_mul(m, m, k->q2inv);
+    z_fdiv_r(m, m, k->p2);
+    z_mul(m, m, k->q2);
+    z_add(m, m, t2);
+    z_fdiv_r(t1, m, k->n2);
+    z_mul(t2, out, t1);
+    z_fdiv_r(out, t2, k->n2);
+    uint32_t* o = b->out + (size_t)i * 2 * nw;
+    memset(o, 0, (size_t)2 * nw * 4);
+    size_t cnt = 0;
+    z_export(o, &cnt, -1, 4, 0, 0, out);
+  }
+  z_clear(out); z_clear(t1); z_clear(t2); z_clear(a); z_clear(m);
+  return NULL;
+}
+
+int gmpb_encrypt_batch(const uint32_t* n, const uint32_t* n2, const uint32_t* p2, const uint32_t* q2,
+                       const uint32_t* q2inv, const uint32_t* hp, const uint32_t* hq, int nw, const uint32_t* m_words,
+                       const uint32_t* a_words, int aw, int64_t count, int threads, uint32_t* out_words) {
+  if (gmpb_load()) return -1;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  key_t_ k;
+  key_init(&k, n, n2, p2, q2, q2inv, hp, hq, nw);
+  pthread_t th[256];
+  batch_t jobs[256];
+  for (int i = 0; i < threads; ++i) {
+    jobs[i] = (batch_t){&k, m_words, a_words, out_words, count, aw, i, threads};
+    pthread_create(&th[i], NULL, batch_worker, &jobs[i]);
+  }
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
   key_clear(&k);
   return 0;
 }

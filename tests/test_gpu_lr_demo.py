@@ -10,9 +10,12 @@ pytestmark = pytest.mark.gpu
 
 
 def test_lr_he_rounds_bit_exact():
+    """One full epoch: 399 training rows = 6 batches of 64 and the 15-row
+    last batch (its mat-vec, noise add and decrypt run other shapes)."""
     from tools.lr_he_demo import run
     from xfl_amd.paillier import PaillierContext
     k = load_fixture(FIXTURES[0])["key"]
     priv = PaillierContext().init(hx(k["p"]), hx(k["q"]), djn_h_pow_n=hx(k["h_pow_n"]))
-    rec = run(epochs=1, check=True, key=priv, max_batches=3)
-    assert rec["batches"] == 3 and rec["checked_bit_exact"] == 3
+    rec = run(epochs=1, check=True, key=priv, per_batch=True)
+    assert rec["batches"] == 7 and rec["checked_bit_exact"] == 7
+    assert [b["rows"] for b in rec["batch_ms"]] == [64] * 6 + [15]

@@ -86,7 +86,7 @@ def _expected_shard(O, okey, rank, step):
     return [O.encrypt_m(okey, O.encode_element(okey, float(x), 7)[0], r) for x, r in zip(xs, rs)]
 
 
-def _pipeline_worker(rank, world, port, q):
+def _pipeline_worker(rank, world, port, q, proxy=None):
     _init(rank, world, port)
     from oracle import paillier_oracle as O
     from xfl_amd._native import ints_to_words
@@ -99,7 +99,7 @@ def _pipeline_worker(rank, world, port, q):
     def produce(i, buf):  # the bench's encode + draw + encrypt, as the oracle computes it
         buf.copy_(torch.from_numpy(ints_to_words(_expected_shard(O, okey, rank, i), n2w).view(np.int32).copy()))
 
-    pipe = GatherPipeline(produce, ROWS, n2w, world=world, rank=rank, device="cpu")
+    pipe = GatherPipeline(produce, ROWS, n2w, world=world, rank=rank, device="cpu", proxy_world=proxy)
     for i in range(5):  # warmup 2 + timed 3 with the double buffer wrapping around
         pipe.step(i)
     pipe.drain()
@@ -115,12 +115,17 @@ def _pipeline_worker(rank, world, port, q):
     other = pipe.vector(last).clone()
     other[rank * ROWS] += 1
     ok_neg = ok_neg and not shard_parity(pipe.shard(last), other, rank, [1], expected)
+    if proxy:  # the gather targets are sized for `proxy` ranks
+        ok_vec = ok_vec and all(g.shape[0] == proxy * ROWS for g in pipe.gathered)
     q.put((rank, (ok_vec, ok_parity, ok_neg)))
     dist.destroy_process_group()
 
 
-def test_bench_pipeline_world2():
-    res = _run(_pipeline_worker, 2)
+@pytest.mark.parametrize("proxy", [None, 8])
+def test_bench_pipeline_world2(proxy):
+    """proxy=8: bench.py --proxy-world, the 8-rank gather volume and target
+    size issued from 2 ranks; the real vector is unaffected."""
+    res = _run(_pipeline_worker, 2, proxy)
     for r, (ok_vec, ok_parity, ok_neg) in res.items():
         assert ok_vec, f"rank {r}: reassembled vector != all ranks' oracle encryptions"
         assert ok_parity and ok_neg, f"rank {r}: shard_parity"

@@ -85,8 +85,12 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, sync_phases=False):
-    """Runs the HE rounds; returns a dict of phase timings and check results."""
+def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, sync_phases=False, per_batch=False,
+        profile_first=False):
+    """Runs the HE rounds; returns a dict of phase timings and check results.
+    per_batch: also a list of every batch's phase times; profile_first: a
+    cProfile of the first epoch's mat-vec calls (top entries by cumulative
+    time) - the diagnosis of the first epoch's one-time costs."""
     from xfl_amd.paillier import Paillier, PaillierContext
     xtr, ytr, _, _ = load_wdbc()
     xl, xt = xtr[:, :15], xtr[:, 15:]
@@ -111,8 +115,14 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
     lr = np.float32(0.01)
     tm = {"encrypt": 0.0, "serialize": 0.0, "matmul": 0.0, "add_noise": 0.0, "decrypt": 0.0}
     epoch_tm = []
+    batch_log = []
+    prof = None
+    if profile_first:
+        import cProfile
+        prof = cProfile.Profile()
     batches = checked = 0
-    for _ in range(epochs):
+    batch_log_prev = {}
+    for ep in range(epochs):
         before = dict(tm)
         nb0 = batches
         for s in range(0, len(xtr), batch):
@@ -134,9 +144,13 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
                              dtype=np.float32)
             noise /= 100000
             a = time.time()
+            if prof is not None and ep == 0:
+                prof.enable()
             g = np.matmul(enc_t, xb_t)
             if sync_phases:
                 _sync()
+            if prof is not None and ep == 0:
+                prof.disable()
             tm["matmul"] += time.time() - a
             a = time.time()
             g = g + noise
@@ -154,6 +168,10 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
                 if not np.array_equal(dec.view(np.uint32), want.view(np.uint32)):
                     raise AssertionError(f"batch {batches}: decrypted gradient differs from the plaintext restatement")
                 checked += 1
+            if per_batch:
+                batch_log.append({"epoch": ep, "rows": int(xb_t.shape[0]),
+                                  **{k: round(1e3 * (tm[k] - (batch_log_prev.get(k, 0.0))), 4) for k in tm}})
+                batch_log_prev = dict(tm)
             gt = np.array(dec, dtype=np.float32) - noise
             gt = -gt / xb_t.shape[0]
             gl = -(resid @ xb_l) / xb_l.shape[0]
@@ -166,6 +184,14 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
            "device_key_s": t_dev, "device_window_bits": priv.device_key().win_bits,
            "phase_s": tm, "he_total_s": sum(tm.values()),
            "per_batch_ms": {k: 1e3 * v / max(batches, 1) for k, v in tm.items()}}
+    if per_batch:
+        rec["batch_ms"] = batch_log
+    if prof is not None:
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+        rec["first_epoch_matmul_profile"] = buf.getvalue()
     if len(epoch_tm) > 1:
         # first epoch carries one-time costs (lazy code-object loads, pools);
         # later epochs are the steady state of a training run
@@ -214,8 +240,11 @@ def main():
     ap.add_argument("--sync-phases", action="store_true",
                     help="synchronise the device at the end of every phase (per-phase latency, diagnostic)")
     ap.add_argument("--cpu-batches", type=int, default=1, help="batches timed through the CPU restatement (0: skip)")
+    ap.add_argument("--per-batch", action="store_true", help="every batch's phase times")
+    ap.add_argument("--profile-first", action="store_true", help="cProfile of the first epoch's mat-vec calls")
     args = ap.parse_args()
-    rec = run(epochs=args.epochs, check=args.check, sync_phases=args.sync_phases)
+    rec = run(epochs=args.epochs, check=args.check, sync_phases=args.sync_phases, per_batch=args.per_batch,
+              profile_first=args.profile_first)
     if args.cpu_batches:
         rec["cpu_restatement_s_per_batch"] = sum(cpu_batch_seconds(seed=i) for i in range(args.cpu_batches)) / \
             args.cpu_batches

@@ -12,6 +12,7 @@ mkdir -p "$OUT"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
   python3 tools/rates_r4.py --only "$OPS" > "$OUT/rates_trace.jsonl" 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 3; }
 for C in "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS" \
          FETCH_SIZE WRITE_SIZE; do
   tag=$(echo "$C" | tr ' ' '_')
   timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$tag" -o pmc --output-format csv -- \

@@ -281,6 +281,13 @@ inline bool modinv_words_binary(const uint32_t* x32, const uint32_t* m32, int nw
 // batches of a few linear passes, instead of ~2 len(m) full-width shift /
 // subtract passes. Returns false when gcd(x, m) != 1; falls back to the plain
 // binary algorithm if the batch budget runs out (never observed).
+// how often modinv_words ran out of its batch budget and took the binary
+// algorithm (a test hook: the batched path is expected to always converge)
+inline int& modinv_fallbacks() {
+  static int n = 0;
+  return n;
+}
+
 inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uint32_t* out32) {
   if (nw32 <= 0 || !(m32[0] & 1)) return modinv_words_binary(x32, m32, nw32, out32);
   const int W = (nw32 + 1) / 2 + 1;
@@ -402,9 +409,11 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
       for (int i = 0; i < nw32; ++i) out32[i] = (uint32_t)(v[i / 2] >> (32 * (i & 1)));
       return true;
     }
-    const int n = std::max(std::max(bitlen(a), bitlen(b)), 128);
+    // the top 64 bits at a common position above the exact low KB bits; when
+    // both fit in 128 bits the u128 holds them whole (the exact binary steps)
+    const int n = std::max(bitlen(a), bitlen(b));
     u128 xa, xb;
-    if (n <= 2 * KB + 2) {  // exact
+    if (n <= 128) {  // exact
       xa = (u128)a[0] | ((u128)(W > 1 ? a[1] : 0) << 64);
       xb = (u128)b[0] | ((u128)(W > 1 ? b[1] : 0) << 64);
     } else {
@@ -442,6 +451,7 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
     u.swap(nu);
     v.swap(nv);
   }
+  ++modinv_fallbacks();  // never observed; tests/test_host_modinv.py asserts it stays 0
   return modinv_words_binary(x32, m32, nw32, out32);
 }
 

@@ -104,40 +104,65 @@ class GatherPipeline:
     collective=True takes the gather path at world 1 too (an initialised
     process group of one rank: bench.py --dist, tests/test_gpu_rccl.py), so
     the RCCL calls of the N-GPU job run on a one-GPU box; the default is
-    world > 1."""
+    world > 1.
 
-    def __init__(self, produce, rows, words, world=1, rank=0, device="cpu", group=None, depth=2, collective=None):
+    proxy_world=P (> world, with the collective): a one-box stand-in for a
+    P-rank job's exchange volume and memory. The gathered vectors are sized
+    for P ranks, and each step issues a second async all-gather that moves
+    the (P - world) / P of the vector the other ranks would send - read from
+    the previous step's vector, written into this step's - so every step
+    carries the P-rank job's gather bytes and RCCL launches next to the
+    kernels (bench.py --proxy-world)."""
+
+    def __init__(self, produce, rows, words, world=1, rank=0, device="cpu", group=None, depth=2, collective=None,
+                 proxy_world=None):
         self.produce = produce
         self.world, self.rank, self.group = world, rank, group
         self.rows = rows
         self.coll = world > 1 if collective is None else bool(collective)
         self.nb = depth if self.coll else 1
+        self.proxy = proxy_world if (self.coll and proxy_world and proxy_world > world) else None
+        vw = self.proxy or world
         self.shards = [torch.empty((rows, words), dtype=torch.int32, device=device) for _ in range(self.nb)]
-        self.gathered = ([torch.empty((world * rows, words), dtype=torch.int32, device=device) for _ in range(self.nb)]
+        self.gathered = ([torch.empty((vw * rows, words), dtype=torch.int32, device=device) for _ in range(self.nb)]
                          if self.coll else None)
+        if self.proxy:
+            assert self.nb >= 2, "the proxy gather reads the previous step's vector"
+            for g in self.gathered:
+                g.zero_()
         self.pending = [None] * self.nb
 
     def step(self, i):
         b = i % self.nb
-        if self.pending[b] is not None:  # the gather still reading shards[b] must finish first
-            self.pending[b].wait()
-            self.pending[b] = None
+        for w in self.pending[b] or ():  # the gathers still reading shards[b] must finish first
+            w.wait()
+        self.pending[b] = None
         buf = self.shards[b]
         self.produce(i, buf)
         if self.coll:
-            self.pending[b] = dist.all_gather_into_tensor(self.gathered[b], buf, group=self.group, async_op=True)
+            w = self.world * self.rows
+            works = [dist.all_gather_into_tensor(self.gathered[b][:w], buf, group=self.group, async_op=True)]
+            if self.proxy:
+                # the other ranks' share of the P-rank vector, read from the
+                # previous step's vector (its gathers were issued earlier on
+                # the same communicator)
+                prev = self.gathered[(i - 1) % self.nb]
+                per = (self.proxy - self.world) * self.rows // self.world
+                works.append(dist.all_gather_into_tensor(self.gathered[b][w:w + per * self.world], prev[:per],
+                                                         group=self.group, async_op=True))
+            self.pending[b] = works
         return buf
 
     def drain(self):
         for b in range(self.nb):
-            if self.pending[b] is not None:
-                self.pending[b].wait()
-                self.pending[b] = None
+            for w in self.pending[b] or ():
+                w.wait()
+            self.pending[b] = None
 
     def vector(self, i):
         """The reassembled vector of step i (after drain); the shard itself without a collective."""
         b = i % self.nb
-        return self.gathered[b] if self.coll else self.shards[b]
+        return self.gathered[b][:self.world * self.rows] if self.coll else self.shards[b]
 
     def shard(self, i):
         return self.shards[i % self.nb]
