@@ -121,6 +121,18 @@ int xhe_multiexp(const xhe_key* key, const uint32_t* bases_dev, int64_t nbases, 
                  const uint32_t* k_dev, int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits,
                  uint32_t* out_dev, void* stream);
 
+/* Row moves of device ciphertext arrays (words per row), the element
+ * selection and assignment of the flat arrays the drop-in returns (fancy
+ * indexing and views of the reference's np.ndarray[object] results,
+ * paillier.py:289-339): gather dst[i] = src[idx[i]] and scatter dst[idx[i]] =
+ * src[i], idx a DEVICE int64 array of count rows (every idx < the row count of
+ * the indexed array; scatter indices distinct). On the device this library
+ * already holds, so no other runtime's kernels are loaded on first use. */
+int xhe_gather_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t count, int words, uint32_t* dst_dev,
+                    void* stream);
+int xhe_scatter_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t count, int words, uint32_t* dst_dev,
+                     void* stream);
+
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
 int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* k,
                       int kw, int kbits, int64_t ncols, int64_t nterms, int win_bits, uint32_t* out);

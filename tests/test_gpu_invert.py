@@ -1,15 +1,10 @@
 """Batch inversion mod n^2 (xhe_invert: PaillierCiphertext._raw_mul's
 invert branch, paillier.py:173-187, utils.py:71-76) across the batch sizes
-of its three shapes - the whole-block product tree (2048-bit keys, up to 256
-elements, k_wtree_*), the same with $XHE_TREE_WAVE=0's single-block 16-lane
-sweeps (a child process: the switch is read once), and the level-by-level
-tree of larger batches - against Python's pow(c, -1, n^2), with odd sizes
-(lone children at every level) and edge residues; a non-invertible element
-fails with XHE_ENOINV."""
-import os
+of its shapes - the whole-block product tree (2048-bit keys, up to 256
+elements, k_wtree_*) and the level-by-level tree of larger batches - against
+Python's pow(c, -1, n^2), with odd sizes (lone children at every level) and
+edge residues; a non-invertible element fails with XHE_ENOINV."""
 import random
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -17,7 +12,6 @@ import pytest
 from tests.conftest import hx, load_fixture
 
 pytestmark = pytest.mark.gpu
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(counts, seed=7):
@@ -53,9 +47,3 @@ def _run(counts, seed=7):
 def test_invert_batch_sizes(counts):
     _run(counts)
 
-
-def test_invert_single_block_sweeps():
-    code = "import sys; sys.path.insert(0, '.'); from tests.test_gpu_invert import _run; _run([1, 3, 64, 255])"
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=dict(os.environ, XHE_TREE_WAVE="0"),
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -7,15 +7,16 @@ c = x y mod N, N = n^2 (K = 4096 bits at 2048-bit keys), 27-bit limbs
 
   T  = x y                                 all 2S columns
   q1 = floor(T / beta^(S-1))               T's limbs S-1 .. 2S-1
-  q2 = q1 mu (mu = floor(beta^(2S) / N))   only columns >= S-1-G (truncated)
+  q2 = q1 mu (mu = floor(beta^(2S) / N))   only columns >= 144 (truncated)
   q3 = floor(q2 / beta^(S+1))
   r  = (T - q3 N) mod beta^(S+1)           only columns <= S of q3 N
   while r >= N: r -= N
 
 Every column is a lazy 64-bit sum of 27x27-bit products (at most S+1 terms
-< 2^54, < 2^62), normalised in rounds of 16 columns (4 lanes x 4 columns) as
-the kernel does: each lane carries its 4 columns locally, hands its carry to
-the next lane, and the round's carry goes to the next round. The model asserts
+< 2^54, < 2^62), normalised in rounds of 32 columns as
+the kernel does (8 lanes x 4 columns per round): each lane carries its 4
+columns locally, hands its carry to the next lane, and the round's carry goes
+to the next round. The model asserts
 every column sum < 2^64 and records how many final subtractions were needed.
 
     python tools/barrett_model.py [trials]
@@ -53,7 +54,12 @@ def columns(a, b, lo, hi):
     return out
 
 
-def normalise_rounds(cols, carry_in=0, round_cols=16, lanes=4):
+LANES = 8          # lanes per element (bar::G)
+ROUND = 4 * LANES  # columns per round
+B0 = 144           # first column of q1 mu computed (bar::B0)
+
+
+def normalise_rounds(cols, carry_in=0, round_cols=ROUND, lanes=LANES):
     """The kernel's normalisation: rounds of lanes x (round_cols/lanes) columns;
     within a lane a sequential carry, then lane to lane, then round to round.
     Returns (limbs, final carry)."""
@@ -90,7 +96,7 @@ def normalise_rounds(cols, carry_in=0, round_cols=16, lanes=4):
     return out, carry
 
 
-def barrett_mul(x, y, N, S, guard=1):
+def barrett_mul(x, y, N, S, lo=B0):
     mu = (1 << (2 * W * S)) // N
     xl, yl = limbs(x, S), limbs(y, S)
     # T = x y: 2S columns, normalised limb by limb
@@ -98,9 +104,8 @@ def barrett_mul(x, y, N, S, guard=1):
     assert c == 0 and value(T) == x * y
     q1 = T[S - 1:2 * S]                      # S+1 limbs
     ml = limbs(mu, S + 1)
-    lo = S - 1 - guard                       # truncated: columns >= lo
-    q2c = columns(q1, ml, lo, 2 * S + 2)
-    pad = (-len(q2c)) % 16
+    q2c = columns(q1, ml, lo, 2 * S + 2)   # truncated: columns >= lo
+    pad = (-len(q2c)) % ROUND
     q2, c2 = normalise_rounds(q2c + [0] * pad)
     q2v = value(q2) + (c2 << (W * len(q2)))  # = floor-truncated q2 / beta^lo
     q3 = q2v >> (W * (S + 1 - lo))
@@ -109,7 +114,7 @@ def barrett_mul(x, y, N, S, guard=1):
     q3l = limbs(q3, S + 1)
     nl = limbs(N, S)
     r2c = columns(q3l, nl, 0, S + 1)
-    pad = (-len(r2c)) % 16
+    pad = (-len(r2c)) % ROUND
     r2, _ = normalise_rounds(r2c + [0] * pad)
     r2 = r2[:S + 1]
     mod = 1 << (W * (S + 1))

@@ -49,6 +49,8 @@ SIGNATURES = {
                                        _vp]),
     "xhe_segprod": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int64, _vp, ctypes.c_int64, _vp, _vp]),
     "xhe_segprod_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int64, _vp, ctypes.c_int64, _vp]),
+    "xhe_gather_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
+    "xhe_scatter_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
     "xhe_multiexp": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_int, _vp, _vp]),
     "xhe_multiexp_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_int,

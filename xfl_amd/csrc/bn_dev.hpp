@@ -77,6 +77,16 @@ XHE_DEV uint64_t mad64s(uint32_t a, uint32_t b_uniform, uint64_t c) {
   return c;
 }
 
+// w[k] for k < nwords, else 0, with no branch: the load index is clamped
+// (nwords >= 1) so every load of an unrolled sequence is in bounds and they
+// all issue back to back. The form `k < nwords ? w[k] : 0` with a runtime
+// nwords compiled to one branch and one s_waitcnt vmcnt(0) per word: the
+// words of a residue were fetched one HBM latency after another (round 5).
+XHE_DEV uint32_t word_or0(const uint32_t* __restrict__ w, int k, int nwords) {
+  const uint32_t v = w[k < nwords ? k : nwords - 1];
+  return k < nwords ? v : 0u;
+}
+
 // ------------------------------------------------------------ lane groups
 // DPP controls: quad_perm [a,b,c,d] = a | b<<2 | c<<4 | d<<6; row_shl:1 0x101
 // (lane i <- lane i+1 of its 16-lane row), row_shr:1 0x111 (lane i <- lane
@@ -975,8 +985,8 @@ struct Mont {
     for (int j = 0; j < L; ++j) {
       const int bit = W * (GG * L + j);
       const int k = bit >> 5, sh = bit & 31;
-      uint32_t lo = k < nwords ? w[k] : 0u;
-      uint32_t hi = (sh + W > 32 && k + 1 < nwords) ? w[k + 1] : 0u;
+      const uint32_t lo = word_or0(w, k, nwords);
+      const uint32_t hi = sh + W > 32 ? word_or0(w, k + 1, nwords) : 0u;
       b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
     }
   }

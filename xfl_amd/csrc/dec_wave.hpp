@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(64 * NWV) k_dec_wave(KeyDev key, const uint32_
     const int n2w = key.n2w;
     for (int j = l; j < 2 * K; j += NT) {
       const int bit = 28 * j, k = bit >> 5, sh = bit & 31;
-      const uint32_t lo = k < n2w ? cw[k] : 0u, hw = k + 1 < n2w ? cw[k + 1] : 0u;
+      const uint32_t lo = word_or0(cw, k, n2w), hw = word_or0(cw, k + 1, n2w);
       s.col[cur][WM::G + j] = (uint32_t)((((uint64_t)hw << 32) | lo) >> sh) & MASK;
     }
   }
@@ -547,7 +547,7 @@ __global__ void __launch_bounds__(64 * NWV) k_mulmod_wave(KeyDev key, const uint
   auto limbs = [&](const uint32_t* wv, uint32_t* dst) {
     for (int i = l; i < K; i += NT) {
       const int bit = WM::W * i, k = bit >> 5, sh = bit & 31;
-      const uint32_t lo = k < key.n2w ? wv[k] : 0u, hi = k + 1 < key.n2w ? wv[k + 1] : 0u;
+      const uint32_t lo = word_or0(wv, k, key.n2w), hi = word_or0(wv, k + 1, key.n2w);
       dst[i] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & MASK;
     }
   };
@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(64 * NWV) k_mulmod_wave(KeyDev key, const uint
 // elements: the LR step's bases with negative coefficients) as a product
 // tree of whole-block WaveMont products, one block per node and one launch
 // per level: the tree's latency is its depth in products (~5 us each), not
-// the 16-lane shape's ~25 us per product (k_tree_up_block/_down_block).
+// the 16-lane shape's ~25 us per product (the round-4 single-block sweeps).
 // Nodes are kept in wave-limb form (K limbs of 27 bits) times R_w; the root
 // leaves in plain words for the host's inverse and comes back the same way.
 template <class WM>
@@ -625,7 +625,7 @@ template <class WM>
 XHE_DEV void wave_limbs_in(const uint32_t* __restrict__ wv, int nwords, uint32_t* dst) {
   for (int i = WM::tid(); i < WM::K_; i += WM::NT) {
     const int bit = WM::W * i, k = bit >> 5, sh = bit & 31;
-    const uint32_t lo = k < nwords ? wv[k] : 0u, hi = k + 1 < nwords ? wv[k + 1] : 0u;
+    const uint32_t lo = word_or0(wv, k, nwords), hi = word_or0(wv, k + 1, nwords);
     dst[i] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & WM::MASK;
   }
 }
@@ -746,354 +746,6 @@ __global__ void __launch_bounds__(64 * NWV) k_wtree_out(KeyDev key, const uint32
   int cur = 0;
   WM::mul(s, cur, s.tl, s.x, false);
   wave_words_out<WM>(s.x, s.zn, key.n2w, words + (size_t)e * key.n2w);
-}
-
-// ---------------------------------------------------------------------------
-// Montgomery DIGITS mod P^2 (pdigit_dev.hpp's PMD: x R^2 = R a + P c mod P^2,
-// K = 37 limbs of 28 bits, R = 2^1036) on whole waves, for the small batches
-// of the LR step. A digit product (a, c) (x) (e, f) is
-//   a' = REDC(a e),  c' = REDC(a f + c e) + (R - 1 - m1) + E
-// (m1 the first REDC's quotient, E = (1 - R) mod P): the same six LDS phases
-// as WaveMont's product, but each phase runs two or three HALF-size (37-limb)
-// column products side by side instead of one 74-limb product - fewer terms
-// per column (3 slices of 16, not 5) and fewer threads per job:
-//   A  T1 = a e, T2 = a f + c e     (3 jobs)
-//   B  T1, T2 mod R normalised      (2 x K threads)
-//   C  m1 = T1 P' mod R, m2 = T2 P' mod R (2 low-only jobs)
-//   D  m1 exactly normalised (carry look-ahead over one wave's ballots: the
-//      (R - 1 - m1) term needs limbs <= MASK), m2 normalised
-//   E  U1 = T1 + m1 P, U2 = T2 + m2 P, and MASK + E_j - m1_j into column K + j
-//      of U2 (that is (R - 1 - m1 + E) R)
-//   F  a' = U1 / R, c' = U2 / R (exact, as WaveMont::tail; c' may exceed R, so
-//      its top limb keeps every bit above it)
-// The REDC quotients are the exact ones, so a' equals the serial kernel's and
-// c' may differ from it by a multiple of P: the same residue (R a + P c mod
-// P^2), and every consumer converts to a canonical residue. Ranges as PMD's:
-// a' < P (1 + 2P/R), c' < R + 4P; the T2 columns (37 products of 28-bit limbs
-// by up to 29-bit limbs, twice) stay below 2^63.
-template <int K, int NWV>
-struct WaveDig {
-  static constexpr int K_ = K;
-  static constexpr int W = 28;
-  static constexpr uint32_t MASK = (1u << W) - 1u;
-  static constexpr int NT = 64 * NWV;
-  static constexpr int TS = 16;
-  static constexpr int NS = (K + TS - 1) / TS;
-  static constexpr int NQF = (2 * K - 1 + 3) / 4, NQL = (K + 3) / 4;
-  static constexpr int JF = NQF * NS, JL = NQL * NS;  // threads of a full / a low-only job
-  static_assert(3 * JF <= NT && 2 * JF + K <= NT, "three full jobs per phase");
-  static_assert(2 * K <= NT && K <= 64, "a limb per thread; m1's look-ahead in one wave");
-  static constexpr int KP = (NS * TS + 3) & ~3;
-  static constexpr int G = 3;
-  static constexpr int ZO = (NS * TS + 4 + 3) & ~3;
-  static constexpr int ZS = (ZO + 4 * NQF + 4 + 3) & ~3;
-  static constexpr int NQ = (2 * K + 3) / 4;  // uint4 quads of an interleaved (a, c) state in HBM
-
-  struct Lds {
-    uint32_t a[KP], c[KP];  // the state (a-operands)
-    uint32_t t1l[KP], t2l[KP], mq1[KP], mq2[KP];
-    uint32_t tab[16][2][KP];  // odd powers (decrypt)
-    uint32_t ze[ZS], zf[ZS];  // the multiplicand (e, f), Z-padded
-    uint32_t zp[ZS], zpp[ZS]; // P and P' = -P^-1 mod R, Z-padded
-    uint32_t topc[KP];        // MASK + E_j
-    uint64_t col1[2][G + 2 * K], col2[2][G + 2 * K];
-    uint64_t mcol1[G + 4 * NQL], mcol2[G + 4 * NQL];
-    uint32_t exw[40];  // the exponent P - 1 (<= 1024 bits)
-  };
-
-  static XHE_DEV int tid() { return (int)threadIdx.x; }
-  static XHE_DEV void sync() { __syncthreads(); }
-  static XHE_DEV uint32_t split3(const uint64_t* cg, int j) {
-    const uint64_t c0 = cg[j], c1 = cg[j - 1], c2 = cg[j - 2];
-    return ((uint32_t)c0 & MASK) + ((uint32_t)(c1 >> W) & MASK) + (uint32_t)(c2 >> (2 * W));
-  }
-  static XHE_DEV uint32_t norm(const uint64_t* cg, int j) { return (split3(cg, j) & MASK) + (split3(cg, j - 1) >> W); }
-
-  // one (quad, slice) of a column product a x z into col (as WaveMont::prodq)
-  template <bool LO>
-  static XHE_DEV void job(int t, const uint32_t* a, const uint32_t* z, uint64_t* col) {
-    constexpr int NQJ = LO ? NQL : NQF;
-    const int q = t % NQJ, sl = t / NQJ;
-    const int t0 = sl * TS;
-    uint4 av[TS / 4], zq[TS / 4 + 1];
-#pragma unroll
-    for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
-    const uint32_t* zb0 = z + (ZO + 4 * q - t0);
-#pragma unroll
-    for (int u = 0; u <= TS / 4; ++u) zq[u] = *reinterpret_cast<const uint4*>(zb0 - 4 * u);
-    uint64_t acc[4] = {0ull, 0ull, 0ull, 0ull};
-#pragma unroll
-    for (int u = 0; u < TS / 4; ++u) {
-      const uint32_t zz[8] = {zq[u + 1].x, zq[u + 1].y, zq[u + 1].z, zq[u + 1].w, zq[u].x, zq[u].y, zq[u].z, zq[u].w};
-      const uint32_t at[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        WaveMont<K, NWV>::mad4(acc, at[r], at[r], at[r], at[r], zz[4 - r], zz[5 - r], zz[6 - r], zz[7 - r]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long*)&col[G + 4 * q + i], (unsigned long long)acc[i]);
-  }
-
-  // U / R from the columns of U (= 0 mod R), limb i of the result (i < K); TOP:
-  // the top limb keeps everything above it (c' may reach 2R)
-  static XHE_DEV uint32_t tail_limb(const uint64_t* cg, int i, bool top) {
-    const uint32_t k = norm(cg, K - 1) != 0u ? 1u : 0u;
-    const uint32_t e0 = (split3(cg, K - 1) >> W) + k;  // into limb 0 of U / R
-    const uint32_t hi = split3(cg, K + i) + (i == 0 ? e0 : 0u);
-    const uint32_t hp = i == 0 ? 0u : split3(cg, K + i - 1) + (i == 1 ? e0 : 0u);
-    if (!top) return (hi & MASK) + (hp >> W);
-    // position 2K of U (column 2K is zero): split3(2K). (Position 2K + 1
-    // would weigh 2^(2W) in this limb: c' < 2^(W K + 2), so it is empty. A
-    // first form still added it as a 32-bit shift by 2W = 56 - undefined, and
-    // the compiler dropped the whole position-2K term with it: c' lost its
-    // bit W K whenever c' >= R, about one product in 4,000.)
-    const uint64_t c1 = cg[2 * K - 1], c2 = cg[2 * K - 2];
-    const uint32_t s2k = ((uint32_t)(c1 >> W) & MASK) + (uint32_t)(c2 >> (2 * W));
-    return hi + (hp >> W) + (s2k << W);
-  }
-
-  // (da, dc) = (pa, pc) (x) (ze, zf); zbw: the result also becomes the next
-  // multiplicand. cur flips (the product goes to the zeroed column buffers).
-  static XHE_DEV void mul(Lds& s, int& cur, const uint32_t* pa, const uint32_t* pc, uint32_t* da, uint32_t* dc,
-                          bool zbw) {
-    cur ^= 1;
-    const int t = tid();
-    // A
-    if (t < JF) job<false>(t, pa, s.ze, s.col1[cur]);
-    else if (t < 2 * JF) job<false>(t - JF, pa, s.zf, s.col2[cur]);
-    else if (t < 3 * JF) job<false>(t - 2 * JF, pc, s.ze, s.col2[cur]);
-    else {
-      for (int i = t - 3 * JF; i < 2 * K; i += NT - 3 * JF) {
-        s.col1[cur ^ 1][G + i] = 0ull;
-        s.col2[cur ^ 1][G + i] = 0ull;
-      }
-    }
-    sync();
-    // B
-    if (t < K) s.t1l[t] = norm(s.col1[cur] + G, t);
-    else if (t < 2 * K) s.t2l[t - K] = norm(s.col2[cur] + G, t - K);
-    else {
-      for (int i = t - 2 * K; i < 4 * NQL; i += NT - 2 * K) {
-        s.mcol1[G + i] = 0ull;
-        s.mcol2[G + i] = 0ull;
-      }
-    }
-    sync();
-    // C
-    if (t < JL) job<true>(t, s.t1l, s.zpp, s.mcol1);
-    else if (t < 2 * JL) job<true>(t - JL, s.t2l, s.zpp, s.mcol2);
-    sync();
-    // D: m1 exact (wave 0), m2 normalised (wave 1)
-    if (t < 64) {
-      const uint32_t v = t < K ? norm(s.mcol1 + G, t) : 0u;  // <= MASK + 2
-      const uint64_t gm = __builtin_amdgcn_ballot_w64(t < K && v > MASK);
-      const uint64_t pm = __builtin_amdgcn_ballot_w64(t < K && v == MASK);
-      const uint64_t ti = gm | pm;
-      const uint64_t cm = (gm + ti) ^ gm ^ ti;  // carries into each limb (as PMDX::normalize_top)
-      if (t < K) s.mq1[t] = (v + (uint32_t)((cm >> t) & 1u)) & MASK;     // limb K-1's carry out: mod R
-    } else if (t - 64 < K) {
-      s.mq2[t - 64] = norm(s.mcol2 + G, t - 64);
-    }
-    sync();
-    // E
-    if (t < JF) job<false>(t, s.mq1, s.zp, s.col1[cur]);
-    else if (t < 2 * JF) job<false>(t - JF, s.mq2, s.zp, s.col2[cur]);
-    else if (t < 2 * JF + K) {
-      const int j = t - 2 * JF;
-      atomicAdd((unsigned long long*)&s.col2[cur][G + K + j], (unsigned long long)(s.topc[j] - s.mq1[j]));
-    }
-    sync();
-    // F
-    if (t < K) {
-      const uint32_t v = tail_limb(s.col1[cur] + G, t, false);
-      da[t] = v;
-      if (zbw) s.ze[ZO + t] = v;
-    } else if (t < 2 * K) {
-      const int i = t - K;
-      const uint32_t v = tail_limb(s.col2[cur] + G, i, i == K - 1);
-      dc[i] = v;
-      if (zbw) s.zf[ZO + i] = v;
-    }
-    sync();
-  }
-};
-
-// digit state (a, c) of one residue <-> interleaved uint4 quads in HBM (the
-// layout of k_dec_pmd_in / _pow / _out: quad q = a_2q, c_2q, a_2q+1, c_2q+1),
-// normalised exactly on the way out (limbs < 2^28, the top limb of c keeps its
-// excess) by one thread
-template <class WD>
-XHE_DEV void wavedig_store(const uint32_t* a, const uint32_t* c, uint4* st, int64_t count) {
-  constexpr int K = WD::K_;
-  uint32_t na[K], nc[K];
-  uint32_t cy = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const uint32_t v = a[j] + cy;
-    na[j] = j + 1 < K ? (v & WD::MASK) : v;
-    cy = v >> WD::W;
-  }
-  cy = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const uint32_t v = c[j] + cy;
-    nc[j] = j + 1 < K ? (v & WD::MASK) : v;
-    cy = v >> WD::W;
-  }
-#pragma unroll
-  for (int q = 0; q < WD::NQ; ++q)
-    st[(size_t)q * count] = make_uint4(2 * q < K ? na[2 * q] : 0u, 2 * q < K ? nc[2 * q] : 0u,
-                                       2 * q + 1 < K ? na[2 * q + 1] : 0u, 2 * q + 1 < K ? nc[2 * q + 1] : 0u);
-}
-
-// x <- x^(P-1) in digits for one residue per block (grid (count, 2)), the
-// digit states of k_dec_pmd_in in and out (st [prime][NQ][count]); the window
-// schedule of k_dec_wave (5-bit sliding window, 16 odd powers in LDS)
-template <int K, int NWV>
-__global__ void __launch_bounds__(64 * NWV) k_dec_wavedig(KeyDev key, int64_t count, uint4* __restrict__ st) {
-  using WD = WaveDig<K, NWV>;
-  constexpr int NT = WD::NT;
-  __shared__ __attribute__((aligned(16))) typename WD::Lds s;
-  const int l = WD::tid();
-  const int prime = blockIdx.y;
-  const int64_t e = blockIdx.x;
-  const ModDev& md = prime ? key.q : key.p;
-  const uint32_t* np = prime ? key.q_nprime37 : key.p_nprime37;
-  const uint32_t* tcg = prime ? key.topc_q : key.topc_p;
-  const uint32_t* ex = prime ? key.qm1_words : key.pm1_words;
-  const int ebits = prime ? key.qm1_bits : key.pm1_bits;
-  {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&s);
-    for (int j = l; j < (int)(sizeof(s) / 4); j += NT) w[j] = 0u;
-  }
-  WD::sync();
-  uint4* se = st + (size_t)prime * WD::NQ * count + e;
-  for (int j = l; j < K; j += NT) {
-    s.zp[WD::ZO + j] = md.N[j];
-    s.zpp[WD::ZO + j] = np[j];
-    s.topc[j] = tcg[j];
-  }
-  for (int q = l; q < WD::NQ; q += NT) {
-    const uint4 v = se[(size_t)q * count];
-    if (2 * q < K) s.a[2 * q] = v.x, s.c[2 * q] = v.y;
-    if (2 * q + 1 < K) s.a[2 * q + 1] = v.z, s.c[2 * q + 1] = v.w;
-  }
-  for (int j = l; j < (ebits + 31) / 32 && j < 40; j += NT) s.exw[j] = ex[j];
-  WD::sync();
-  auto copy2 = [&](uint32_t* da, uint32_t* dc, const uint32_t* pa, const uint32_t* pc, int zo) {
-    for (int j = l; j < K; j += NT) {
-      da[zo + j] = pa[j];
-      dc[zo + j] = pc[j];
-    }
-  };
-  auto bit = [&](int i) { return (s.exw[i >> 5] >> (i & 31)) & 1u; };
-  int cur = 0;
-  // tab[0] = x; x^2 (kept as the multiplicand); tab[t] = tab[t-1] x^2
-  copy2(s.tab[0][0], s.tab[0][1], s.a, s.c, 0);
-  copy2(s.ze, s.zf, s.a, s.c, WD::ZO);
-  WD::sync();
-  WD::mul(s, cur, s.a, s.c, s.a, s.c, true);
-#pragma unroll 1
-  for (int t = 1; t < 16; ++t) WD::mul(s, cur, s.tab[t - 1][0], s.tab[t - 1][1], s.tab[t][0], s.tab[t][1], false);
-  int i = ebits - 1;
-  while (i >= 0 && !bit(i)) --i;
-  {  // the first window's odd power is the start value
-    int j = i - 4 < 0 ? 0 : i - 4;
-    while (!bit(j)) ++j;
-    uint32_t val = 0;
-    for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
-    copy2(s.a, s.c, s.tab[val >> 1][0], s.tab[val >> 1][1], 0);
-    copy2(s.ze, s.zf, s.tab[val >> 1][0], s.tab[val >> 1][1], WD::ZO);
-    i = j - 1;
-  }
-  WD::sync();
-  int pend_sq = 0, pend_mul = -1;
-#pragma unroll 1
-  while (true) {
-    if (pend_sq > 0) {
-      WD::mul(s, cur, s.a, s.c, s.a, s.c, true);  // (e, f) = (a, c): the square
-      --pend_sq;
-    } else if (pend_mul >= 0) {
-      copy2(s.ze, s.zf, s.tab[pend_mul][0], s.tab[pend_mul][1], WD::ZO);
-      WD::sync();
-      WD::mul(s, cur, s.a, s.c, s.a, s.c, false);
-      copy2(s.ze, s.zf, s.a, s.c, WD::ZO);  // the next squaring's multiplicand
-      WD::sync();
-      pend_mul = -1;
-    } else if (i < 0) {
-      break;
-    } else if (!bit(i)) {
-      pend_sq = 1;
-      --i;
-    } else {
-      int j = i - 4 < 0 ? 0 : i - 4;
-      while (!bit(j)) ++j;
-      uint32_t val = 0;
-      for (int k = i; k >= j; --k) val = (val << 1) | bit(k);
-      pend_sq = i - j + 1;
-      pend_mul = (int)(val >> 1);
-      i = j - 1;
-    }
-  }
-  if (l == 0) wavedig_store<WD>(s.a, s.c, se, count);
-}
-
-// DJN fixed-base products h^a mod P^2 in digits for small batches (the LR
-// step's 64-element encrypt): one block per (element, prime), the window
-// rows (packed digit pairs, k_djn_pmd's tables) unpacked into the
-// multiplicand, 1 digit product per window; the digit state out for
-// k_nodjn_pmd_out ((1 + n m) folded on the way to the rows k_crt_enc reads).
-template <int K, int NWV, int RW>
-__global__ void __launch_bounds__(64 * NWV) k_djn_wavedig(KeyDev key, const uint32_t* __restrict__ a_words, int aw,
-                                                          int64_t count, uint4* __restrict__ st) {
-  using WD = WaveDig<K, NWV>;
-  constexpr int NT = WD::NT, HW = RW / 2;
-  __shared__ __attribute__((aligned(16))) typename WD::Lds s;
-  const int l = WD::tid();
-  const int prime = blockIdx.y;
-  const int64_t e = blockIdx.x;
-  const ModDev& md = prime ? key.q : key.p;
-  const uint32_t* np = prime ? key.q_nprime37 : key.p_nprime37;
-  const uint32_t* tcg = prime ? key.topc_q : key.topc_p;
-  const uint32_t* tab = prime ? key.tab_q2 : key.tab_p2;
-  const uint32_t* ae = a_words + (size_t)e * aw;
-  {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&s);
-    for (int j = l; j < (int)(sizeof(s) / 4); j += NT) w[j] = 0u;
-  }
-  WD::sync();
-  for (int j = l; j < K; j += NT) {
-    s.zp[WD::ZO + j] = md.N[j];
-    s.zpp[WD::ZO + j] = np[j];
-    s.topc[j] = tcg[j];
-  }
-  // limb j of the packed half-row h (HW words) of table row `row`
-  auto limb = [&](const uint32_t* row, int h, int j) -> uint32_t {
-    const int bit = WD::W * j, k = bit >> 5, sh = bit & 31;
-    const uint32_t lo = k < HW ? row[h * HW + k] : 0u, hi = k + 1 < HW ? row[h * HW + k + 1] : 0u;
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & WD::MASK;
-  };
-  int cur = 0;
-  for (int w = 0; w < key.nwin; ++w) {
-    int64_t row0;
-    const uint32_t d = win_digit(key, ae, aw, w, row0);
-    const uint32_t* row = tab + (size_t)(row0 + d) * key.tab_rs;
-    if (w == 0) {
-      for (int j = l; j < K; j += NT) {
-        s.a[j] = limb(row, 0, j);
-        s.c[j] = limb(row, 1, j);
-      }
-      WD::sync();
-      continue;
-    }
-    for (int j = l; j < 2 * K; j += NT) {
-      if (j < K) s.ze[WD::ZO + j] = limb(row, 0, j);
-      else s.zf[WD::ZO + j - K] = limb(row, 1, j - K);
-    }
-    WD::sync();
-    WD::mul(s, cur, s.a, s.c, s.a, s.c, false);
-  }
-  if (l == 0) wavedig_store<WD>(s.a, s.c, st + (size_t)prime * WD::NQ * count + e, count);
 }
 
 }  // namespace xhe

@@ -643,10 +643,32 @@ struct PMDX {
     else if constexpr (TPI == 2) return G::template dpp<k | (k << 2) | ((2 + k) << 4) | ((2 + k) << 6)>(v);
     else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);  // row_newbcast
   }
+  // (k a constant after unrolling: the dispatch folds away)
   XHE_DEV static uint32_t from_lane_i(uint32_t v, int k) {
-    static_assert(TPI == 4 || TPI == 2, "");
+    static_assert(TPI == 4 || TPI == 2 || TPI == 16, "");
     if constexpr (TPI == 2) return k == 0 ? from_lane<0>(v) : from_lane<1>(v);
-    else return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
+    else if constexpr (TPI == 4)
+      return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
+    else {
+      switch (k) {
+        case 0: return from_lane<0>(v);
+        case 1: return from_lane<1>(v);
+        case 2: return from_lane<2>(v);
+        case 3: return from_lane<3>(v);
+        case 4: return from_lane<4>(v);
+        case 5: return from_lane<5>(v);
+        case 6: return from_lane<6>(v);
+        case 7: return from_lane<7>(v);
+        case 8: return from_lane<8>(v);
+        case 9: return from_lane<9>(v);
+        case 10: return from_lane<10>(v);
+        case 11: return from_lane<11>(v);
+        case 12: return from_lane<12>(v);
+        case 13: return from_lane<13>(v);
+        case 14: return from_lane<14>(v);
+        default: return from_lane<15>(v);
+      }
+    }
   }
 
   // REDC with the quotient digits kept: T (lazy K-limb columns per lane) +
@@ -724,8 +746,8 @@ XHE_DEV void limbs_at(uint32_t (&b)[L], const uint32_t* __restrict__ w, int nwor
 #pragma unroll
   for (int j = 0; j < L; ++j) {
     const int bit = W * (FIRST + j), k = bit >> 5, sh = bit & 31;
-    const uint32_t lo = k < nwords ? w[k] : 0u;
-    const uint32_t hi = (sh + W > 32 && k + 1 < nwords) ? w[k + 1] : 0u;
+    const uint32_t lo = word_or0(w, k, nwords);
+    const uint32_t hi = sh + W > 32 ? word_or0(w, k + 1, nwords) : 0u;
     b[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << W) - 1u);
   }
 }

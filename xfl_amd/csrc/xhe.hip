@@ -20,6 +20,7 @@
 #include "hostbn.hpp"
 #include "xhe_kernels.hpp"
 #include "dec_wave.hpp"
+#include "barrett_dev.hpp"
 
 using namespace xhe;
 
@@ -88,6 +89,11 @@ struct Shape8192 {
   using MP = Mont<152, 27, 4>;
   using MN2 = Mont<640, 26, 16>;
   using MN2X = Mont<640, 26, 16>;
+  // Montgomery digits mod p^2, q^2 (4096-bit primes: 160 limbs of 27 bits,
+  // R = 2^4320), one 16-lane row per residue (10 limbs per lane) for the
+  // products and the conversions alike (round 5)
+  using PDX = PMDX<160, 16>;
+  using PDXO = PMDX<160, 16>;
 };
 
 // XHE_ONLY_BITS=K (XHE_ONLY_2048 = 2048): a development build with one key
@@ -328,7 +334,13 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
   size_t o_nlim = bl.put_limbs(n, k->mp2);
   ModOff o_n2m = put_mod(bl, n2, k->mn2, kRpowRows);
   ModOff o_n2X = put_mod(bl, n2, k->mn2X, kRpowRows);
-  size_t o_n2wN = 0, o_n2wnp = 0, o_n2wC = 0, o_n2wR2 = 0;
+  size_t o_n2wN = 0, o_n2wnp = 0, o_n2wC = 0, o_n2wR2 = 0, o_n2mu = 0;
+  if (K == 2048) {  // k_add_barrett: mu = floor(beta^(2S) / n^2), beta = 2^27, S = 152
+    static_assert(bar::S == 152, "Barrett constants are for 2048-bit keys");
+    BigU mu;
+    divmod(pow2((size_t)27 * 2 * bar::S), n2, &mu, nullptr);
+    o_n2mu = bl.put_limbs(mu, ModSpec{bar::S + 1, 27});
+  }
   if (K == 2048) {  // k_mexp_horner_wave
     const ModSpec sw{154, 27};
     const BigU Rw = pow2((size_t)27 * 154), RX = pow2((size_t)k->mn2X.W * k->mn2X.S);
@@ -400,7 +412,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t pm1 = 0, qm1 = 0, pinv = 0, qinv = 0, hpR = 0, hqR = 0, qinvpR = 0, q_lim = 0, p2x = 0, p_lim = 0;
     size_t ep = 0, eq = 0;
     size_t topc_p = 0, topc_q = 0;
-    size_t nprime_p2 = 0, nprime_q2 = 0, nprime37_p = 0, nprime37_q = 0;
+    size_t nprime_p2 = 0, nprime_q2 = 0;
     ModOff xd[2];
     size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
     size_t xdw[2] = {0, 0}, xhpR[2] = {0, 0};
@@ -495,19 +507,16 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       };
       o.topc_p = topc(P);
       o.topc_q = topc(Q);
-      // -P^-1 mod R for the whole-wave digit kernels (WaveDig)
-      o.nprime37_p = bl.put(sub(T, modinv(mod(P, T), T)).to_limbs(28, 37));
-      o.nprime37_q = bl.put(sub(T, modinv(mod(Q, T), T)).to_limbs(28, 37));
     }
 #endif
 #if XHE_PMDX
-    if (K == 3072 || K == 4096) {
+    if (K == 3072 || K == 4096 || K == 8192) {
       // Montgomery digits mod P^2 over 4 lanes (k_djn_pmdx, k_dec_pmdx_*): per
       // prime the modulus P in K limbs of 27 bits (R = 2^(27 K)), ceil(R/P)
       // P^2, R - P, MASK + E_i, the fold constant Q R^3 mod P, the digits of
       // R^2 R_MP2^-1 mod P^2 (R_MP2: the MP2 shape's R, the tables' factor)
       // and of R^2 mod P^2 (plain conversion), and hp R mod P (decrypt)
-      const int KD = K == 3072 ? 60 : 80;
+      const int KD = K == 3072 ? 60 : K == 4096 ? 80 : 160;
       const ModSpec sd{KD, 27};
       const BigU Rd = pow2((size_t)27 * KD), RM = pow2((size_t)s2.W * s2.S);
       for (int i = 0; i < 2; ++i) {
@@ -578,6 +587,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     kd.n2w_np = B + o_n2wnp;
     kd.n2w_C = B + o_n2wC;
     kd.n2w_R2 = B + o_n2wR2;
+    kd.n2_mu = B + o_n2mu;
   }
   kd.nR2_n2 = B + o_nR2n2;
   kd.n_bits = (int)n.bits();
@@ -639,12 +649,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     if (K == 2048) {
       kd.topc_p = B + o.topc_p;
       kd.topc_q = B + o.topc_q;
-      kd.p_nprime37 = B + o.nprime37_p;
-      kd.q_nprime37 = B + o.nprime37_q;
     }
 #endif
 #if XHE_PMDX
-    if (K == 3072 || K == 4096) {
+    if (K == 3072 || K == 4096 || K == 8192) {
       kd.pmdx_dec = 1;
       kd.x_dw_p = reinterpret_cast<const uint2*>(B + o.xdw[0]);
       kd.x_dw_q = reinterpret_cast<const uint2*>(B + o.xdw[1]);
@@ -701,13 +709,13 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       }
 #endif
 #if XHE_PMDX
-      if (K == 3072 || K == 4096) {
+      if (K == 3072 || K == 4096 || K == 8192) {
         // rows as Montgomery digits (e, f) for k_djn_pmdx
         kd.pmdx = 1;
         const int64_t trows = (int64_t)(kd.nwin + kd.nhi) << kd.win;
         with_shape(K, [&](auto sh) {
           using Sh = decltype(sh);
-          if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+          if constexpr (Sh::K == 3072 || Sh::K == 4096 || Sh::K == 8192) {
             using D = typename Sh::PDXO;
             for (int i = 0; i < 2; ++i) {
               hipLaunchKernelGGL((k_tab_to_pmdx<D, Sh::RW>), dim3((unsigned)((trows * D::TPI + 127) / 128)),
@@ -866,20 +874,6 @@ void crt_enc_launch(const xhe_key* k, int64_t n, uint32_t* ws, uint32_t* ct, hip
   HIPCHK(hipGetLastError());
 }
 
-// Whole-wave digit kernels for the smallest 2048-bit batches (k_djn_wavedig
-// up to kEncWaveMax elements, k_dec_wavedig for the decrypt's wave regime),
-// opt-in with $XHE_WAVEDIG=1: measured slower than k_dec_wave (15-element
-// decrypt 3.29 vs 2.27 ms) and no faster end to end than k_djn_pmd<16> for
-// the LR step's 64-element encrypt.
-constexpr int64_t kEncWaveMax = 256;
-bool wavedig_on() {
-  static const bool on = [] {
-    const char* e = getenv("XHE_WAVEDIG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 // lanes per element of k_djn_pmd: 16 up to 2 k elements, 4 up to 16 k, else
 // 1 (the chip holds ~128 k one-lane residues: 2 waves x 1024 SIMDs x 64);
 // $XHE_PMD_SPLIT pins it (1, 4 or 16)
@@ -905,26 +899,6 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     int blocks = (int)((n * MP2::TPI + 255) / 256);
 #if XHE_PMD && XHE_LDS_ROWS
     if constexpr (Sh::K == 2048) {
-      if (k->kd.pmd && n <= kEncWaveMax && wavedig_on()) {
-        // the smallest batches: one 4-wave block per (element, prime), the
-        // fixed-base products as whole-wave digit products (k_djn_wavedig),
-        // then (1 + n m) folded on the way to the rows (k_nodjn_pmd_out)
-        using WD = WaveDig<37, 4>;
-        uint4* st = nullptr;
-        ws_alloc((void**)&st, (size_t)2 * WD::NQ * n * sizeof(uint4), s);
-        {
-          ProfScope ps("k_djn_pmd", s);
-          hipLaunchKernelGGL((k_djn_wavedig<37, 4, Sh::RW>), dim3((unsigned)n, 2), dim3(256), 0, s, k->kd,
-                             r + (size_t)off * k->rand_words, k->rand_words, n, st);
-          HIPCHK(hipGetLastError());
-        }
-        hipLaunchKernelGGL((k_nodjn_pmd_out<MP2, 37>), dim3((unsigned)((n + 127) / 128), 2), dim3(128), 0, s, k->kd,
-                           k->kd.p.N, k->kd.q.N, k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, n, st, ws);
-        HIPCHK(hipGetLastError());
-        ws_free(st, s);
-        crt_enc_launch<Sh>(k, n, ws, ct + (size_t)off * k->n2w, s);
-        continue;
-      }
       if (k->kd.pmd) {
         ProfScope ps("k_djn_pmd", s);
         // small batches split each element's windows over G lanes (latency:
@@ -945,7 +919,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
     }
 #endif
 #if XHE_PMDX
-    if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+    if constexpr (Sh::K == 3072 || Sh::K == 4096 || Sh::K == 8192) {
       if (k->kd.pmdx) {
         using D = typename Sh::PDX;
         if (!xst) {
@@ -1263,11 +1237,13 @@ bool add_wave_on() {
   return on;
 }
 
-// Small-batch inversion as a tree of whole-block products (k_wtree_*);
-// $XHE_TREE_WAVE=0 keeps the single-block 16-lane sweeps (A/B).
-bool tree_wave_on() {
+
+// Equal-exponent adds of 2048-bit ciphertexts in the 4-lane regime run the
+// one-product Barrett kernel (k_add_barrett); $XHE_ADD_BAR=0 keeps the
+// Montgomery pair (k_mulmod_n2) for the A/B.
+bool add_bar_on() {
   static const bool on = [] {
-    const char* e = getenv("XHE_TREE_WAVE");
+    const char* e = getenv("XHE_ADD_BAR");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1280,6 +1256,16 @@ void mulmod_impl(const xhe_key* k, const uint32_t* a, const int32_t* ea, const u
     if (count <= kWaveAddMax && dmax >= kWaveAddMinD && add_wave_on()) {
       hipLaunchKernelGGL((k_mulmod_wave<154, 16>), dim3((unsigned)count), dim3(1024), 0, s, k->kd, a, ea, b, eb, count,
                          out, eout);
+      HIPCHK(hipGetLastError());
+      return;
+    }
+  }
+  if constexpr (Sh::K == 2048 && MN2::TPI == 4) {
+    if (dmax == 0 && add_bar_on()) {
+      ProfScope ps("k_add_barrett", s);
+      const int64_t blocks = (count + bar::EPB - 1) / bar::EPB;
+      hipLaunchKernelGGL(k_add_barrett, dim3((unsigned)blocks), dim3(bar::TPB), 0, s, k->kd, a, ea, b, eb, count, out,
+                         eout);
       HIPCHK(hipGetLastError());
       return;
     }
@@ -1351,7 +1337,7 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
     tot += (size_t)S4 * n;
   }
   if constexpr (Sh::K == 2048 && MN2::TPI == 16) {  // (a 1024-thread block: the 16-lane 2048-bit shape's registers)
-  if (count <= 256 && tree_wave_on()) {
+  if (count <= 256) {
     // small batch: a product tree of whole-block products (dec_wave.hpp
     // k_wtree_*), one launch per level
     constexpr int KW = 154;
@@ -1399,45 +1385,6 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
     (void)hipFreeAsync(lv, s);
     (void)hipFreeAsync(inv, s);
     (void)hipFreeAsync(wds, s);
-    return XHE_OK;
-  }
-  if (count <= 256) {
-    // small batch: one block per sweep (k_tree_up_block / k_tree_down_block)
-    const int nlev = (int)sizes.size();
-    std::vector<int64_t> plan(2 * nlev);
-    for (int l = 0; l < nlev; ++l) {
-      plan[l] = (int64_t)offs[l];
-      plan[nlev + l] = sizes[l];
-    }
-    uint32_t *lv = nullptr, *inv = nullptr, *wds = nullptr;
-    int64_t* dplan = nullptr;
-    HIPCHK(hipMallocAsync((void**)&lv, tot * 4, s));
-    HIPCHK(hipMallocAsync((void**)&inv, tot * 4, s));
-    HIPCHK(hipMallocAsync((void**)&wds, (size_t)2 * k->n2w * 4, s));
-    HIPCHK(hipMallocAsync((void**)&dplan, plan.size() * 8, s));
-    HIPCHK(hipMemcpyAsync(dplan, plan.data(), plan.size() * 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_tree_up_block<MN2>, dim3(1), dim3(1024), 0, s, k->kd, n2h<MN2>(k).N, c, count, lv, dplan,
-                       dplan + nlev, nlev, wds);
-    HIPCHK(hipGetLastError());
-    std::vector<uint32_t> root(k->n2w), yinv(k->n2w);
-    HIPCHK(hipMemcpyAsync(root.data(), wds, (size_t)k->n2w * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));  // (plan and root copies done)
-    if (!modinv_words(root.data(), k->n2_host.data(), k->n2w, yinv.data())) {
-      (void)hipFreeAsync(lv, s);
-      (void)hipFreeAsync(inv, s);
-      (void)hipFreeAsync(wds, s);
-      (void)hipFreeAsync(dplan, s);
-      return fail(XHE_ENOINV, "invert(a, b) no inverse exists");
-    }
-    HIPCHK(hipMemcpyAsync(wds + k->n2w, yinv.data(), (size_t)k->n2w * 4, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_tree_down_block<MN2>, dim3(1), dim3(1024), 0, s, k->kd, n2h<MN2>(k).N, wds + k->n2w, lv, inv,
-                       dplan, dplan + nlev, nlev, out);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));  // yinv is host memory of this frame
-    (void)hipFreeAsync(lv, s);
-    (void)hipFreeAsync(inv, s);
-    (void)hipFreeAsync(wds, s);
-    (void)hipFreeAsync(dplan, s);
     return XHE_OK;
   }
   }
@@ -1857,7 +1804,7 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
     int64_t n = std::min(chunk, count - off);
     const uint32_t* cto = ct + (size_t)off * k->n2w;
 #if XHE_PMDX
-    if constexpr (Sh::K == 3072 || Sh::K == 4096) {
+    if constexpr (Sh::K == 3072 || Sh::K == 4096 || Sh::K == 8192) {
       if (k->kd.pmdx_dec && dec_pmdx_on() && (pin ? pin == 1 : tpi == 4)) {
         // batches: digits (the 16-lane shape keeps the small ones)
         dec_pmdx_launch<Sh>(k, cto, n, chunk, mrows, s);
@@ -1871,28 +1818,6 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
 #endif
     if (tpi == 64) {
       if constexpr (wave_ok) {
-#if XHE_PMD && XHE_LDS_ROWS
-        if (wavedig_on()) {
-          // digits: k_dec_pmd_in (c -> digits), x^(P-1) on whole-wave digit
-          // products (k_dec_wavedig), k_dec_pmd_out (-> X_P rows)
-          constexpr int NQ = PMD<37>::NQ;
-          uint4* st = nullptr;
-          ws_alloc((void**)&st, (size_t)2 * NQ * n * sizeof(uint4), s);
-          const dim3 g1((unsigned)((n + 127) / 128), 2);
-          hipLaunchKernelGGL((k_dec_pmd_in<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
-                             k->kd.q2.N, cto, k->n2w, n, st);
-          HIPCHK(hipGetLastError());
-          {
-            ProfScope ps("k_dec_wave", s);
-            hipLaunchKernelGGL((k_dec_wavedig<37, 4>), dim3((unsigned)n, 2), dim3(256), 0, s, k->kd, n, st);
-            HIPCHK(hipGetLastError());
-          }
-          hipLaunchKernelGGL((k_dec_pmd_out<MP2, 37>), g1, dim3(128), 0, s, k->kd, k->kd.p.N, k->kd.q.N, k->kd.p2.N,
-                             k->kd.q2.N, n, st, (int)MP2::S4, xrows);
-          HIPCHK(hipGetLastError());
-          ws_free(st, s);
-        } else
-#endif
         {
         static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave shares the MP2 limbs");
         ProfScope ps("k_dec_wave", s);
@@ -2267,6 +2192,19 @@ void rand_impl(const xhe_key* key, const uint8_t* seed32, uint64_t nonce, int64_
   HIPCHK(hipGetLastError());
 }
 }  // namespace
+
+// row gather (SCATTER = false: dst[i] = src[idx[i]]) or scatter (dst[idx[i]] =
+// src[i]), one word per thread, grid-stride (xhe_gather_rows / xhe_scatter_rows)
+template <bool SCATTER>
+__global__ void k_move_rows(const uint32_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t count,
+                            int words, uint32_t* __restrict__ dst) {
+  const int64_t tot = count * words;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / words, w = t - i * words;
+    if (SCATTER) dst[idx[i] * words + w] = src[t];
+    else dst[t] = src[idx[i] * words + w];
+  }
+}
 
 extern "C" {
 
@@ -2711,6 +2649,36 @@ int xhe_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int xhe_gather_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t count, int words, uint32_t* dst_dev,
+                    void* stream) {
+  return guarded([&]() -> int {
+    if (count < 0 || words <= 0) return fail(XHE_EINVAL, "xhe_gather_rows: bad size");
+    if (count == 0) return XHE_OK;
+    if (!src_dev || !idx_dev || !dst_dev) return fail(XHE_EINVAL, "xhe_gather_rows: null argument");
+    const int64_t tot = count * words;
+    const unsigned blocks = (unsigned)std::min<int64_t>((tot + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_move_rows<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src_dev, idx_dev, count,
+                       words, dst_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
+}
+
+int xhe_scatter_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t count, int words, uint32_t* dst_dev,
+                     void* stream) {
+  return guarded([&]() -> int {
+    if (count < 0 || words <= 0) return fail(XHE_EINVAL, "xhe_scatter_rows: bad size");
+    if (count == 0) return XHE_OK;
+    if (!src_dev || !idx_dev || !dst_dev) return fail(XHE_EINVAL, "xhe_scatter_rows: null argument");
+    const int64_t tot = count * words;
+    const unsigned blocks = (unsigned)std::min<int64_t>((tot + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_move_rows<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src_dev, idx_dev, count,
+                       words, dst_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
 }
 
 int xhe_synchronize(void* stream) {

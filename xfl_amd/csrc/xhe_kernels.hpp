@@ -112,9 +112,9 @@ struct KeyDev {
   // keys): n^2 in 154 limbs of 27 bits (R_w = 2^4158), -n^-2 mod R_w and
   // C = R_w^2 R_X^-1 mod n^2 (R_X = 2^(27*160): the 16-lane shape's R)
   const uint32_t *n2w_N, *n2w_np, *n2w_C, *n2w_R2;  // (R2: R_w^2 mod n^2, k_mulmod_wave)
-  // ---- Montgomery digits on whole waves (WaveDig, 2048-bit keys): -P^-1 mod
-  // R (R = 2^(28*37)) as 37 limbs, per prime
-  const uint32_t *p_nprime37, *q_nprime37;
+  // ---- Barrett reduction mod n^2 (k_add_barrett, 2048-bit keys):
+  // floor(2^(27*304) / n^2) as 153 limbs of 27 bits
+  const uint32_t* n2_mu;
 };
 
 // ============================================================== encode
@@ -397,7 +397,7 @@ XHE_DEV void unpack_limbs_lds(uint32_t* slot) {
 // straddle two words; bits beyond nwords read as zero)
 XHE_DEV uint32_t digit_at(const uint32_t* w, int nwords, int bit, int win) {
   int k = bit >> 5, sh = bit & 31;
-  uint64_t v = (uint64_t)(k < nwords ? w[k] : 0u) | ((uint64_t)(k + 1 < nwords ? w[k + 1] : 0u) << 32);
+  uint64_t v = (uint64_t)word_or0(w, k, nwords) | ((uint64_t)word_or0(w, k + 1, nwords) << 32);
   return (uint32_t)(v >> sh) & ((1u << win) - 1u);
 }
 
@@ -993,7 +993,7 @@ __global__ void __launch_bounds__(256, 2) k_p2_reduce_words(KeyDev key, const ui
     for (int j = 0; j < MP2L::L; ++j) {
       const int J = MP2L::S + g * MP2L::L + j;
       const int bit = MP2L::W * J, k = bit >> 5, sh = bit & 31;
-      const uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+      const uint32_t lo = word_or0(cw, k, n2w), h2 = word_or0(cw, k + 1, n2w);
       sq[(size_t)(g * MP2L::L + j) * st] = (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2L::MASK;
     }
     if (g == 0)
@@ -1185,7 +1185,7 @@ __global__ void __launch_bounds__(128, 2) k_dec_pmd_in(KeyDev key, const uint32_
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int J = MP2::S + 4 * q + r, bit = MP2::W * J, k = bit >> 5, sh = bit & 31;
-        const uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+        const uint32_t lo = word_or0(cw, k, n2w), h2 = word_or0(cw, k + 1, n2w);
         v[r] = 4 * q + r < MP2::S ? (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2::MASK : 0u;
       }
       *reinterpret_cast<uint4*>(slot + q * 256) = make_uint4(v[0], v[1], v[2], v[3]);
@@ -1375,7 +1375,7 @@ __global__ void __launch_bounds__(256, 2) k_tab_to_pmd(const uint32_t* __restric
 #pragma unroll
   for (int l = 0; l < 2 * KP; ++l) {
     const int bit = 28 * l, k = bit >> 5, sh = bit & 31;
-    const uint32_t lo = k < RW ? w[k] : 0u, hi = k + 1 < RW ? w[k + 1] : 0u;
+    const uint32_t lo = word_or0(w, k, RW), hi = word_or0(w, k + 1, RW);
     X[l] = __builtin_amdgcn_alignbit(hi, lo, sh) & ((1u << 28) - 1u);
   }
   PMD<KP> M;
@@ -1647,7 +1647,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_pow(KeyDev key, const uint32_t* 
       for (int j = 0; j < MP2::L; ++j) {
         int J = MP2::S + g * MP2::L + j;
         int bit = MP2::W * J, k = bit >> 5, sh = bit & 31;
-        uint32_t lo = k < n2w ? cw[k] : 0u, h2 = k + 1 < n2w ? cw[k + 1] : 0u;
+        uint32_t lo = word_or0(cw, k, n2w), h2 = word_or0(cw, k + 1, n2w);
         sq[(size_t)(g * MP2::L + j) * st] = (uint32_t)((((uint64_t)h2 << 32) | lo) >> sh) & MP2::MASK;
       }
       if (g == 0)
@@ -1793,7 +1793,7 @@ XHE_DEV void pow_window4(const M_& M, uint32_t (&b)[M_::L], const uint32_t* R1, 
 XHE_DEV uint32_t nibble(const uint32_t* w, int nwords, int win) {
   int bit = win * 4;
   int k = bit >> 5;
-  return k < nwords ? (w[k] >> (bit & 31)) & 15u : 0u;
+  return (word_or0(w, k, nwords) >> (bit & 31)) & 15u;
 }
 
 // out = a * b mod n^2 after aligning exponents: the operand with the larger
@@ -2377,95 +2377,6 @@ __global__ void __launch_bounds__(256, 2) k_from_mont_rows(KeyDev key, const uin
   M.mul(b, AOne{});
   M.reduce_once(b);
   store_packed(M, b, rows + e, (int)count, out + (size_t)e * key.n2w, key.n2w);
-}
-
-// Small batches (<= one block of lane groups): the whole up-sweep in ONE
-// launch - to Montgomery rows, every tree level (__syncthreads between
-// levels; the levels' rows in global memory, offsets lvo[l] and sizes lvn[l]
-// host-planned as for k_tree_up) and the root packed to words - and the whole
-// down-sweep in another (root inverse to a row, every level, out of
-// Montgomery form). A batch inversion of the LR step's 64 bases took 16
-// launches of one 16-lane product each (the launch gaps, not the products,
-// were most of its ~0.3 ms).
-template <class MN2>
-__global__ void __launch_bounds__(1024) k_tree_up_block(KeyDev key, const uint32_t* __restrict__ Nn2,
-                                                        const uint32_t* __restrict__ c, int64_t count,
-                                                        uint32_t* __restrict__ lv, const int64_t* __restrict__ lvo,
-                                                        const int64_t* __restrict__ lvn, int nlev,
-                                                        uint32_t* __restrict__ root_words) {
-  const int groups = (int)(blockDim.x / MN2::TPI);
-  const int g = (int)(threadIdx.x / MN2::TPI);
-  MN2 M;
-  M.init(Nn2, n2dev<MN2>(key).n0inv);
-  uint32_t b[MN2::L];
-  for (int64_t e = g; e < count; e += groups) {
-    M.load_words(b, c + (size_t)e * key.n2w, key.n2w);
-    M.mul(b, ARow{n2dev<MN2>(key).R2});
-    M.reduce_once(b);
-    M.store_strided(b, lv + e, (int)count);
-  }
-  __syncthreads();
-  for (int l = 1; l < nlev; ++l) {
-    const int64_t n_in = lvn[l - 1], n_out = lvn[l];
-    const uint32_t* in = lv + lvo[l - 1];
-    uint32_t* outp = lv + lvo[l];
-    for (int64_t i = g; i < n_out; i += groups) {
-      M.load_strided(b, in + 2 * i, (int)n_in);
-      if (2 * i + 1 < n_in) {
-        M.mul(b, AStrided{in + 2 * i + 1, (int)n_in});
-        M.reduce_once(b);
-      }
-      M.store_strided(b, outp + i, (int)n_out);
-    }
-    __syncthreads();
-  }
-  if (g == 0) pack_words_<MN2::W, MN2::TPI>(lv + lvo[nlev - 1], 1, MN2::S, root_words, key.n2w);
-}
-
-template <class MN2>
-__global__ void __launch_bounds__(1024) k_tree_down_block(KeyDev key, const uint32_t* __restrict__ Nn2,
-                                                          const uint32_t* __restrict__ y_words,
-                                                          const uint32_t* __restrict__ lv, uint32_t* __restrict__ inv,
-                                                          const int64_t* __restrict__ lvo,
-                                                          const int64_t* __restrict__ lvn, int nlev,
-                                                          uint32_t* __restrict__ out) {
-  const int groups = (int)(blockDim.x / MN2::TPI);
-  const int g = (int)(threadIdx.x / MN2::TPI);
-  MN2 M;
-  M.init(Nn2, n2dev<MN2>(key).n0inv);
-  uint32_t b[MN2::L];
-  if (g == 0) {  // (P R)^-1 words -> P^-1 R (as k_inv_to_row)
-    M.load_words(b, y_words, key.n2w);
-    M.mul(b, ARow{n2dev<MN2>(key).R3});
-    M.reduce_once(b);
-    M.store_strided(b, inv + lvo[nlev - 1], 1);
-  }
-  __syncthreads();
-  for (int l = nlev - 1; l >= 1; --l) {
-    const int64_t n_par = lvn[l], n_child = lvn[l - 1];
-    const uint32_t* pinv = inv + lvo[l];
-    const uint32_t* child = lv + lvo[l - 1];
-    uint32_t* cinv = inv + lvo[l - 1];
-    for (int64_t i = g; i < n_child; i += groups) {
-      M.load_strided(b, pinv + i / 2, (int)n_par);
-      const int64_t sib = i ^ 1;
-      if (sib < n_child) {
-        M.mul(b, AStrided{child + sib, (int)n_child});
-        M.reduce_once(b);
-      }
-      M.store_strided(b, cinv + i, (int)n_child);
-    }
-    __syncthreads();
-  }
-  const int64_t count = lvn[0];
-  for (int64_t e = g; e < count; e += groups) {
-    M.load_strided(b, inv + e, (int)count);
-    M.mul(b, AOne{});
-    M.reduce_once(b);
-    M.store_strided(b, const_cast<uint32_t*>(lv) + e, (int)count);  // the level-0 rows are free now: pack scratch
-    wave_sync_mem_();
-    pack_words_<MN2::W, MN2::TPI>(lv + e, (int)count, MN2::S, out + (size_t)e * key.n2w, key.n2w);
-  }
 }
 
 // Root of the product tree <-> plain words for k_inv_single (one group).

@@ -383,18 +383,39 @@ def multiexp(dk, bases, idx, kw_, kbits, win_bits=0):
 
 
 def take(c, idx):
-    """rows of device c at host indices idx (a new tensor)"""
+    """rows of device c at host indices idx (a new tensor; xhe_gather_rows, so
+    no torch kernel is loaded on first use - a first index_select of a new
+    shape class cost 75 ms in the LR step's 15-row batch)"""
     torch = _torch()
     dev = c.device.index
-    ii = upload(np.ascontiguousarray(idx, dtype=np.int64), dev)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
     with _On(dev):
-        return torch.index_select(c, 0, ii)
+        out = torch.empty((idx.shape[0],) + tuple(c.shape[1:]), dtype=c.dtype, device=c.device)
+    if idx.shape[0]:
+        ii = upload(idx, dev)
+        nat.check(nat.lib().xhe_gather_rows(_dp(c), _dp(ii), idx.shape[0], _row_words(c), _dp(out), _sp(dev)),
+                  "gather_rows")
+    return out
 
 
 def cat(parts):
+    """rows of the parts one after another (copies, no concatenation kernel)"""
     torch = _torch()
     with _On(parts[0].device.index):
-        return torch.cat(parts, 0)
+        out = torch.empty((sum(p.shape[0] for p in parts),) + tuple(parts[0].shape[1:]), dtype=parts[0].dtype,
+                          device=parts[0].device)
+        off = 0
+        for p in parts:
+            out[off:off + p.shape[0]].copy_(p)
+            off += p.shape[0]
+    return out
+
+
+def _row_words(c):
+    n = 1
+    for d in c.shape[1:]:
+        n *= int(d)
+    return n
 
 
 def clone(c):
@@ -403,9 +424,11 @@ def clone(c):
 
 
 def put_rows(c, idx, rows):
-    """c[idx] = rows (device) in place"""
-    torch = _torch()
+    """c[idx] = rows (device) in place (xhe_scatter_rows; idx distinct)"""
     dev = c.device.index
-    ii = upload(np.ascontiguousarray(idx, dtype=np.int64), dev)
-    with _On(dev):
-        c.index_copy_(0, ii, rows)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    if idx.shape[0]:
+        ii = upload(idx, dev)
+        src = rows.contiguous()
+        nat.check(nat.lib().xhe_scatter_rows(_dp(src), _dp(ii), idx.shape[0], _row_words(c), _dp(c), _sp(dev)),
+                  "scatter_rows")
