@@ -7,7 +7,7 @@ c = x y mod N, N = n^2 (K = 4096 bits at 2048-bit keys), 27-bit limbs
 
   T  = x y                                 all 2S columns
   q1 = floor(T / beta^(S-1))               T's limbs S-1 .. 2S-1
-  q2 = q1 mu (mu = floor(beta^(2S) / N))   only columns >= 144 (truncated)
+  q2 = q1 mu (mu = floor(beta^(2S) / N))   only columns >= 148 (truncated)
   q3 = floor(q2 / beta^(S+1))
   r  = (T - q3 N) mod beta^(S+1)           only columns <= S of q3 N
   while r >= N: r -= N
@@ -56,7 +56,7 @@ def columns(a, b, lo, hi):
 
 LANES = 8          # lanes per element (bar::G)
 ROUND = 4 * LANES  # columns per round
-B0 = 144           # first column of q1 mu computed (bar::B0)
+B0 = 148           # first column of q1 mu computed (bar::B0 = S - 4)
 
 
 def normalise_rounds(cols, carry_in=0, round_cols=ROUND, lanes=LANES):

@@ -6,7 +6,7 @@
 // 27-bit limbs, S = 152 (N < beta^S, N >= beta^(S-1), beta = 2^27):
 //   A  T  = x y                 304 columns (S^2 = 23.1 k mads)
 //   B  q3 = floor(floor(T / beta^(S-1)) mu / beta^(S+1)), mu = floor(beta^2S / N),
-//          from the columns >= 144 of q1 mu only (~12 k mads)
+//          from the columns 148 .. 307 of q1 mu only (~12 k mads)
 //   C  r2 = q3 N mod beta^160   columns < 160 (~12 k mads)
 //   D  r  = (T - r2) mod beta^160 = T - q3 N (< 4N), then r -= N while r >= N
 // ~47 k mads against 2 x 2 S^2 = 92.4 k for the Montgomery pair, and no
@@ -92,13 +92,32 @@ XHE_DEV void mad_block(uint64_t (&acc)[4], const uint4& x, const uint4& w03, uin
       : "vcc");
 }
 
+// The operands of one pair of 4-term blocks (terms i0 .. i0+7)
+struct Pair {
+  uint4 ya, xa, yb, xb;  // y_{c-i0-3 .. c-i0}, x_{i0 .. i0+3}, y_{c-i0-7 .. c-i0-4}, x_{i0+4 .. i0+7}
+};
+XHE_DEV Pair load_pair(const uint32_t* yp, const uint32_t* xp, int p) {
+  Pair q;
+  q.ya = *reinterpret_cast<const uint4*>(yp - 8 * p);
+  q.xa = *reinterpret_cast<const uint4*>(xp + 8 * p);
+  q.yb = *reinterpret_cast<const uint4*>(yp - 8 * p - 4);
+  q.xb = *reinterpret_cast<const uint4*>(xp + 8 * p + 4);
+  return q;
+}
+// the pair's 32 mads; w4..w6 = y_{c-i0+1 .. c-i0+3}
+XHE_DEV void mad_pair(uint64_t (&acc)[4], const Pair& q, uint32_t w4, uint32_t w5, uint32_t w6) {
+  mad_block(acc, q.xa, q.ya, w4, w5, w6);
+  mad_block(acc, q.xb, q.yb, q.ya.x, q.ya.y, q.ya.z);
+}
+
 // lane g's column sums acc[k] = sum_i x_i y_{C0 + 4g + k - i} over the terms
 // of columns [C0, C0 + 4G): x at xr[i] (LX limbs, zeros to XLEN), y at
 // yr[YOFF + j] (LY limbs, zero-padded). Terms go in pairs of 4-term blocks
 // (the range rounded up to a multiple of 8 with zero x), so the window's two
-// halves alternate roles with no register moves but the 3 carried limbs; the
-// loop is not unrolled further (unrolled, the compiler hoisted every LDS read
-// of a round and spilled).
+// halves alternate roles, and two pairs per iteration carry the window in
+// each other's registers (no moves). Loading a pair ahead measured no faster
+// (the kernel is VALU-issue-bound, 93 % busy). Not unrolled further:
+// unrolled, the compiler hoisted every LDS read of a round and spilled.
 XHE_DEV void cols(const uint32_t* xr, const uint32_t* yr, int C0, int g, int LX, int LY, uint64_t (&acc)[4]) {
   int ilo = C0 - (LY - 1);
   ilo = ilo < 0 ? 0 : ilo;
@@ -115,16 +134,23 @@ XHE_DEV void cols(const uint32_t* xr, const uint32_t* yr, int C0, int g, int LX,
   const uint32_t* yp = yr + YOFF - 3 + c - ib0;  // y_{c-i0-3} at yp[-(i0 - ib0)]
   const uint32_t* xp = xr + ib0;
 #pragma unroll 1
-  for (int p = 0; p < npair; ++p) {
-    const uint4 ya = *reinterpret_cast<const uint4*>(yp - 8 * p);      // y_{c-i0-3} .. y_{c-i0}
-    const uint4 xa = *reinterpret_cast<const uint4*>(xp + 8 * p);      // x_{i0} .. x_{i0+3}
-    const uint4 yb = *reinterpret_cast<const uint4*>(yp - 8 * p - 4);  // y_{c-i0-7} .. y_{c-i0-4}
-    const uint4 xb = *reinterpret_cast<const uint4*>(xp + 8 * p + 4);  // x_{i0+4} .. x_{i0+7}
-    mad_block(acc, xa, ya, w4, w5, w6);
-    mad_block(acc, xb, yb, ya.x, ya.y, ya.z);
-    w4 = yb.x;
-    w5 = yb.y;
-    w6 = yb.z;
+  for (int p = 0; p < npair; p += 2) {
+    // two pairs per iteration, the window carried in the other pair's
+    // registers (no moves); the second pair is skipped (wave-uniform) when
+    // the count is odd
+    const Pair A = load_pair(yp, xp, p);
+    mad_pair(acc, A, w4, w5, w6);
+    if (p + 1 < npair) {
+      const Pair B = load_pair(yp, xp, p + 1);
+      mad_pair(acc, B, A.yb.x, A.yb.y, A.yb.z);
+      w4 = B.yb.x;
+      w5 = B.yb.y;
+      w6 = B.yb.z;
+    } else {
+      w4 = A.yb.x;
+      w5 = A.yb.y;
+      w6 = A.yb.z;
+    }
   }
 }
 
@@ -247,9 +273,11 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
       if (t >= S - 1 && t < 2 * S) xr[t - (S - 1)] = T[r][k];
     }
   for (int j = S + 1 + g; j < XLEN; j += G) xr[j] = 0u;
-  // ---- B: q3 = the limbs >= S+1 of q1 mu, from its columns >= 144 (>= S-1-7)
-  constexpr int B0 = 144, RB = (2 * (S + 1) + 2 - B0 + RCOLS - 1) / RCOLS;
-  static_assert(B0 % 4 == 0 && B0 <= S - 2, "truncation guard");
+  // ---- B: q3 = the limbs >= S+1 of q1 mu, from its columns 148 .. 307
+  // (>= S-1-3: the truncation costs q3 at most 1, tools/barrett_model.py;
+  // q1 mu has no column above 2S, + its carry)
+  constexpr int B0 = S - 4, RB = (2 * S + 2 - B0 + RCOLS - 1) / RCOLS;
+  static_assert(B0 % 4 == 0 && B0 + RB * RCOLS >= 2 * S + 2, "truncation guard and top columns");
   rc = 0;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
@@ -263,6 +291,9 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
       if (t >= 0 && t < XLEN) yr[t] = l[k];                // x-role layout (y is no longer needed)
     }
   }
+  // q3's x-role row ends in zeros (limbs 153, 154 were written as the zero
+  // columns 306, 307; what lies beyond is y's old window)
+  for (int j = S + 1 + g; j < XLEN; j += G) yr[j] = 0u;
   // ---- C: r2 = q3 N mod beta^(4G * RC)
   constexpr int RC = (S + 1 + RCOLS - 1) / RCOLS;
   uint32_t R2[RC][4];
