@@ -298,7 +298,7 @@ XHE_DEV void rand_elem(const ChaChaKey& ck, int64_t i, int words, int bits, cons
   if (status) *status = ST_VALUE;
 }
 
-__global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
+__global__ void __launch_bounds__(256) k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
                              const uint32_t* __restrict__ bound, uint32_t* __restrict__ out,
                              int32_t* __restrict__ status) {
   const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -313,8 +313,11 @@ __global__ void k_rand_below(ChaChaKey ck, int64_t base, int64_t count, int word
 // rows. The same stream and the same words as k_rand_below: attempt 0 is the
 // draw unless it is zero (probability 2^-bits), which the group's ballot
 // detects and the group's first lane redraws from attempt 1 on.
-__global__ void k_rand_djn(ChaChaKey ck, int64_t base, int64_t count, int words, int bits, int tpe,
-                           uint32_t* __restrict__ out, int32_t* __restrict__ status) {
+// (launched with 256 threads: without the bound the compiler assumed
+// 1,024-thread blocks, capped the kernel at 128 VGPRs and spilled 262 of
+// them around the rare redraw path)
+__global__ void __launch_bounds__(256) k_rand_djn(ChaChaKey ck, int64_t base, int64_t count, int words, int bits,
+                                                  int tpe, uint32_t* __restrict__ out, int32_t* __restrict__ status) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t li = t / tpe;
   const int b = (int)(t & (tpe - 1));
