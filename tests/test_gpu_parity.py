@@ -122,7 +122,7 @@ def test_decrypt_shapes_bit_exact(fx, count):
     assert out == (ms * reps)[:count]
 
 
-@pytest.mark.parametrize("count", [7, 700])
+@pytest.mark.parametrize("count", [7, 300, 700])
 def test_decrypt_arbitrary_residues(count):
     """Any c < n^2 coprime to n (as every ciphertext is), not only
     well-formed ciphertexts, decrypts as the reference's arithmetic does
