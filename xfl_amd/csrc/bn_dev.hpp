@@ -1,7 +1,7 @@
 // Device multi-precision Montgomery arithmetic for gfx950 (CDNA4).
 //
 // Representation: a residue mod M is S limbs of W bits (W = 27/28) held one
-// limb per 32-bit VGPR. A group of TPI consecutive lanes (TPI in {1,2,4,16})
+// limb per 32-bit VGPR. A group of TPI consecutive lanes (TPI in {1,2,4,8,16})
 // owns one residue, lane g holding limbs [g*L, (g+1)*L), L = S/TPI.
 //
 // The Montgomery product is operand scanning with LAZY carries: the running
@@ -93,8 +93,11 @@ XHE_DEV uint32_t word_or0(const uint32_t* __restrict__ w, int k, int nwords) {
 // i-1), row_newbcast:k 0x150+k (lane k of the row to the whole row, gfx90a+).
 template <int TPI>
 struct Grp {
-  static_assert(TPI == 1 || TPI == 2 || TPI == 4 || TPI == 16, "lane groups of 1, 2, 4 or 16");
+  static_assert(TPI == 1 || TPI == 2 || TPI == 4 || TPI == 8 || TPI == 16, "lane groups of 1, 2, 4, 8 or 16");
   static XHE_DEV int g() { return TPI == 1 ? 0 : (int)(threadIdx.x & (TPI - 1)); }
+  // 8-lane groups are half rows: a row control reaches both halves, and
+  // the upper half (lanes 8-15 of the row) takes the value meant for it
+  static XHE_DEV bool upper8() { return (threadIdx.x & 8) != 0; }
 
   // (mov_dpp with bound_ctrl: a source lane outside the 16-lane row reads 0,
   // and no "old" value has to be materialised first)
@@ -107,20 +110,29 @@ struct Grp {
     if constexpr (TPI == 1) return v;
     else if constexpr (TPI == 2) return dpp<0xA0>(v);
     else if constexpr (TPI == 4) return dpp<0x00>(v);
-    else return dpp<0x150>(v);
+    else if constexpr (TPI == 8) {
+      const uint32_t r0 = dpp<0x150>(v), r8 = dpp<0x158>(v);  // row_newbcast:0, :8
+      return upper8() ? r8 : r0;
+    } else return dpp<0x150>(v);
   }
   // value held by the last lane of the group
   static XHE_DEV uint32_t bcast_last(uint32_t v) {
     if constexpr (TPI == 1) return v;
     else if constexpr (TPI == 2) return dpp<0xF5>(v);
     else if constexpr (TPI == 4) return dpp<0xFF>(v);
-    else return dpp<0x15F>(v);
+    else if constexpr (TPI == 8) {
+      const uint32_t r7 = dpp<0x157>(v), r15 = dpp<0x15F>(v);
+      return upper8() ? r15 : r7;
+    } else return dpp<0x15F>(v);
   }
   // value held by lane g+1 (0 for the last lane)
   static XHE_DEV uint32_t from_next(uint32_t v) {
     if constexpr (TPI == 1) return 0u;
     else if constexpr (TPI == 16) return dpp<0x101>(v);  // lane 15 reads outside the row: 0
-    else {
+    else if constexpr (TPI == 8) {
+      const uint32_t r = dpp<0x101>(v);  // row_shl:1; lane 7 of the row reads lane 8
+      return g() == 7 ? 0u : r;
+    } else {
       uint32_t r = TPI == 2 ? dpp<0xF5>(v) : dpp<0xF9>(v);
       return g() == TPI - 1 ? 0u : r;
     }
@@ -129,7 +141,10 @@ struct Grp {
   static XHE_DEV uint32_t from_prev(uint32_t v) {
     if constexpr (TPI == 1) return 0u;
     else if constexpr (TPI == 16) return dpp<0x111>(v);  // lane 0 reads outside the row: 0
-    else {
+    else if constexpr (TPI == 8) {
+      const uint32_t r = dpp<0x111>(v);  // row_shr:1; lane 8 of the row reads lane 7
+      return g() == 0 ? 0u : r;
+    } else {
       uint32_t r = TPI == 2 ? dpp<0xA0>(v) : dpp<0x90>(v);
       return g() == 0 ? 0u : r;
     }
@@ -731,7 +746,8 @@ struct Mont {
         all &= (b[j] == MASK) ? 1u : 0u;
         __builtin_amdgcn_sched_barrier(0);
       }
-      constexpr uint64_t top = TPI == 16 ? 0x8000800080008000ull : 0x8888888888888888ull;
+      constexpr uint64_t top = TPI == 16 ? 0x8000800080008000ull : TPI == 8 ? 0x8080808080808080ull
+                                                                            : 0x8888888888888888ull;
       const uint64_t gm = __builtin_amdgcn_ballot_w64(cin != 0) & ~top;
       const uint64_t tm = (gm | __builtin_amdgcn_ballot_w64(all != 0)) & ~top;
       const uint64_t cm = (gm + tm) ^ gm ^ tm;

@@ -618,8 +618,8 @@ struct PMDX {
       all &= (b[j] == MASK) ? 1u : 0u;
     }
     // generate: cin (0 or 1) leaves the lane; propagate: all limbs MASK
-    constexpr uint64_t tops = TPI == 16 ? 0x8000800080008000ull : TPI == 4 ? 0x8888888888888888ull
-                                                                            : 0xAAAAAAAAAAAAAAAAull;
+    constexpr uint64_t tops = TPI == 16 ? 0x8000800080008000ull : TPI == 8 ? 0x8080808080808080ull
+                              : TPI == 4 ? 0x8888888888888888ull : 0xAAAAAAAAAAAAAAAAull;
     const uint64_t gm = __builtin_amdgcn_ballot_w64(cin != 0);
     const uint64_t pm = __builtin_amdgcn_ballot_w64(all != 0);
     const uint64_t gi = gm & ~tops, ti = (gm | pm) & ~tops;
@@ -641,15 +641,30 @@ struct PMDX {
   XHE_DEV static uint32_t from_lane(uint32_t v) {
     if constexpr (TPI == 4) return G::template dpp<k | (k << 2) | (k << 4) | (k << 6)>(v);
     else if constexpr (TPI == 2) return G::template dpp<k | (k << 2) | ((2 + k) << 4) | ((2 + k) << 6)>(v);
-    else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);  // row_newbcast
+    else if constexpr (TPI == 8) {  // half rows: lane k of each half
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x158 + k, 0xF, 0xF, true);
+      return G::upper8() ? hi : lo;
+    } else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + k, 0xF, 0xF, true);  // row_newbcast
   }
   // (k a constant after unrolling: the dispatch folds away)
   XHE_DEV static uint32_t from_lane_i(uint32_t v, int k) {
-    static_assert(TPI == 4 || TPI == 2 || TPI == 16, "");
+    static_assert(TPI == 4 || TPI == 2 || TPI == 8 || TPI == 16, "");
     if constexpr (TPI == 2) return k == 0 ? from_lane<0>(v) : from_lane<1>(v);
     else if constexpr (TPI == 4)
       return k == 0 ? from_lane<0>(v) : k == 1 ? from_lane<1>(v) : k == 2 ? from_lane<2>(v) : from_lane<3>(v);
-    else {
+    else if constexpr (TPI == 8) {
+      switch (k) {
+        case 0: return from_lane<0>(v);
+        case 1: return from_lane<1>(v);
+        case 2: return from_lane<2>(v);
+        case 3: return from_lane<3>(v);
+        case 4: return from_lane<4>(v);
+        case 5: return from_lane<5>(v);
+        case 6: return from_lane<6>(v);
+        default: return from_lane<7>(v);
+      }
+    } else {
       switch (k) {
         case 0: return from_lane<0>(v);
         case 1: return from_lane<1>(v);

@@ -59,6 +59,7 @@ struct Shape3072 {
   using MN2X = Mont<240, 27, 16>;
   using PDX = PMDX<60, 2>;   // Montgomery digits mod p^2, q^2: k_djn_pmdx's products (2 lanes of 30 limbs)
   using PDXO = PMDX<60, 4>;  // its conversions (k_pmdx_enc_out, k_tab_to_pmdx; 2 lanes would spill there)
+  using PDXP = PMDX<60, 4>;  // the decrypt exponentiation (2 lanes spill 70 VGPRs in pmdx_pow_uniform)
 };
 // 4096-bit keys (the LR/LinReg/Pearson/WoE operators' OneOf(2048, 4096, 8192)):
 // 28-bit limbs would overflow the lazy 64-bit accumulator at S = 147
@@ -76,6 +77,7 @@ struct Shape4096 {
   using MN2X = Mont<304, 27, 16>;
   using PDX = PMDX<80, 4>;
   using PDXO = PMDX<80, 4>;
+  using PDXP = PMDX<80, 4>;
 };
 
 // 8192-bit keys: p^2 (8192 bits) in one 16-lane row of 27-bit limbs, p in 4
@@ -90,10 +92,12 @@ struct Shape8192 {
   using MN2 = Mont<640, 26, 16>;
   using MN2X = Mont<640, 26, 16>;
   // Montgomery digits mod p^2, q^2 (4096-bit primes: 160 limbs of 27 bits,
-  // R = 2^4320), one 16-lane row per residue (10 limbs per lane) for the
-  // products and the conversions alike (round 5)
-  using PDX = PMDX<160, 16>;
+  // R = 2^4320): the products (encrypt and decrypt exponentiations) on half
+  // rows, 8 lanes of 20 limbs (no spills: 170 / 230 VGPRs); the conversions
+  // on whole 16-lane rows (8 lanes spill 44 VGPRs in k_pmdx_enc_out)
+  using PDX = PMDX<160, 8>;
   using PDXO = PMDX<160, 16>;
+  using PDXP = PMDX<160, 8>;
 };
 
 // XHE_ONLY_BITS=K (XHE_ONLY_2048 = 2048): a development build with one key
@@ -1744,7 +1748,7 @@ template <class Sh>
 void dec_pmdx_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t chunk, uint32_t* mrows,
                      hipStream_t s) {
   using DO = typename Sh::PDXO;  // conversions (register room)
-  using DP = typename Sh::PDXO;  // the exponentiation (2 lanes spill 70 VGPRs in pmdx_pow_uniform at 3072)
+  using DP = typename Sh::PDXP;  // the exponentiation
   using MP2L = typename Sh::MP2L;
   using MP = typename Sh::MP;
   constexpr int RW = Sh::RW, NWH = Sh::K / 64;
