@@ -137,6 +137,12 @@ struct Grp {
       return g() == TPI - 1 ? 0u : r;
     }
   }
+  // value held by lane g+1; the last lane's is unspecified (no mask)
+  static XHE_DEV uint32_t from_next_any(uint32_t v) {
+    if constexpr (TPI == 1) return 0u;
+    else if constexpr (TPI == 16 || TPI == 8) return dpp<0x101>(v);
+    else return TPI == 2 ? dpp<0xF5>(v) : dpp<0xF9>(v);
+  }
   // value held by lane g-1 (0 for lane 0)
   static XHE_DEV uint32_t from_prev(uint32_t v) {
     if constexpr (TPI == 1) return 0u;

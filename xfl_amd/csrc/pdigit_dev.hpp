@@ -502,6 +502,31 @@ struct PMDX {
     }
   }
 
+  // one position of both accumulators in one asm statement (the tail past
+  // the 4-limb blocks; separate mad statements each cost a hazard nop)
+  template <bool SQ>
+  XHE_DEV void blk1(uint64_t (&T1)[L], uint64_t (&T2)[L], const uint32_t (&a)[L], const uint32_t (&c)[L],
+                    uint32_t e, uint32_t f, uint32_t m1, uint32_t m2, int j) const {
+    if constexpr (SQ) {  // f carries 2e
+      asm("v_mad_u64_u32 %0, vcc, %4, %6, %2\n\t"
+          "v_mad_u64_u32 %1, vcc, %5, %7, %3\n\t"
+          "v_mad_u64_u32 %0, vcc, %8, %10, %0\n\t"
+          "v_mad_u64_u32 %1, vcc, %9, %10, %1"
+          : "+v"(T1[j - 1]), "+v"(T2[j - 1])
+          : "v"(T1[j]), "v"(T2[j]), "v"(e), "v"(f), "v"(a[j]), "v"(c[j]), "v"(m1), "v"(m2), "v"(M.nl[j])
+          : "vcc");
+    } else {
+      asm("v_mad_u64_u32 %0, vcc, %4, %6, %2\n\t"
+          "v_mad_u64_u32 %1, vcc, %4, %7, %3\n\t"
+          "v_mad_u64_u32 %0, vcc, %8, %10, %0\n\t"
+          "v_mad_u64_u32 %1, vcc, %5, %6, %1\n\t"
+          "v_mad_u64_u32 %1, vcc, %9, %10, %1"
+          : "+v"(T1[j - 1]), "+v"(T2[j - 1])
+          : "v"(T1[j]), "v"(T2[j]), "v"(e), "v"(f), "v"(a[j]), "v"(c[j]), "v"(m1), "v"(m2), "v"(M.nl[j])
+          : "vcc");
+    }
+  }
+
   // one step of the two interleaved reductions (see PMD::step); entry: x1 =
   // T1[0] + e a[0], x2 = T2[0] + e c[0] + f a[0] (or 2e c[0]) and the
   // broadcast digits m1, m2; the next step's x and m are formed under this
@@ -512,8 +537,12 @@ struct PMDX {
                     uint32_t e, uint32_t f, uint32_t en, uint32_t fn, uint32_t& m1, uint32_t& m2, uint64_t& x1,
                     uint64_t& x2, uint32_t topc) const {
     static_assert(L >= 8, "positions 1..L-1: 4-limb blocks and a tail");
-    const uint64_t v1 = mad64(m1, M.nl[0], x1);  // lane 0: = 0 (mod 2^W)
-    const uint64_t v2 = mad64(m2, M.nl[0], x2);
+    uint64_t v1, v2;  // v1 = x1 + m1 n_0 (lane 0: = 0 mod 2^W), v2 likewise, one statement
+    asm("v_mad_u64_u32 %0, vcc, %2, %4, %5\n\t"
+        "v_mad_u64_u32 %1, vcc, %3, %4, %6"
+        : "=&v"(v1), "=v"(v2)
+        : "v"(m1), "v"(m2), "v"(M.nl[0]), "v"(x1), "v"(x2)
+        : "vcc");
     // the limbs handed down to lane g-1 (DPP sources well before the DPP)
     const uint32_t h1 = (uint32_t)v1 & MASK, h2 = (uint32_t)v2 & MASK;
     const uint32_t f2 = SQ ? (e << 1) : f;
@@ -526,15 +555,26 @@ struct PMDX {
         T2[0] += v2 >> W;
         asm volatile("" : "+v"(T1[0]), "+v"(T2[0]));
       } else if (stage == 1) {
-        x1n = mad64(en, a[0], T1[0]);
-        if constexpr (SQ) x2n = mad64(en << 1, c[0], T2[0]);
-        else x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
+        if constexpr (SQ) {
+          asm("v_mad_u64_u32 %0, vcc, %2, %3, %5\n\t"
+              "v_mad_u64_u32 %1, vcc, %4, %7, %6"
+              : "=&v"(x1n), "=v"(x2n)
+              : "v"(en), "v"(a[0]), "v"(en << 1), "v"(T1[0]), "v"(T2[0]), "v"(c[0])
+              : "vcc");
+        } else {
+          asm("v_mad_u64_u32 %0, vcc, %2, %4, %6\n\t"
+              "v_mad_u64_u32 %1, vcc, %2, %5, %7\n\t"
+              "v_mad_u64_u32 %1, vcc, %3, %4, %1"
+              : "=&v"(x1n), "=&v"(x2n)
+              : "v"(en), "v"(fn), "v"(a[0]), "v"(c[0]), "v"(T1[0]), "v"(T2[0])
+              : "vcc");
+        }
         asm volatile("" : "+v"(x1n), "+v"(x2n));
       } else if (stage == 2) {
         t1 = (uint32_t)x1n * M.n0inv;
         t2 = (uint32_t)x2n * M.n0inv;
         d1 = G::from_next(h1);
-        d2 = G::from_next(h2);
+        d2 = G::from_next_any(h2);  // (the last lane takes topc - m1 instead)
         asm volatile("" : "+v"(t1), "+v"(t2), "+v"(d1), "+v"(d2));
       } else if (stage == 3) {
         t1 = G::bcast0(t1 & MASK);
@@ -551,11 +591,7 @@ struct PMDX {
       advance();
     }
 #pragma unroll
-    for (; j < L; ++j) {  // the tail
-      T1[j - 1] = mad64(m1, M.nl[j], mad64(e, a[j], T1[j]));
-      if constexpr (SQ) T2[j - 1] = mad64(m2, M.nl[j], mad64(f2, c[j], T2[j]));
-      else T2[j - 1] = mad64(m2, M.nl[j], mad64(f, a[j], mad64(e, c[j], T2[j])));
-    }
+    for (; j < L; ++j) blk1<SQ>(T1, T2, a, c, e, f2, m1, m2, j);  // the tail
     while (stage < 4) advance();
     T1[L - 1] = d1;
     T2[L - 1] = last() ? (uint64_t)(topc - m1) : (uint64_t)d2;
