@@ -51,72 +51,88 @@ struct PMD {
     n0inv = ninv;
   }
 
-  // T1[j-1+k] = T1[j+k] + e a[j+k] + m P[j+k], k = 0..5 (tied accumulators:
-  // T1[j-1+k] is written after T1[j-1+k]'s old value was consumed)
-  XHE_DEV void blk1(uint64_t (&T)[K], const uint32_t (&a)[K], uint32_t e, uint32_t m, int j) const {
-    asm("v_mad_u64_u32 %0, vcc, %7, %9, %1\n\t"
-        "v_mad_u64_u32 %1, vcc, %7, %10, %2\n\t"
-        "v_mad_u64_u32 %2, vcc, %7, %11, %3\n\t"
-        "v_mad_u64_u32 %3, vcc, %7, %12, %4\n\t"
-        "v_mad_u64_u32 %4, vcc, %7, %13, %5\n\t"
-        "v_mad_u64_u32 %5, vcc, %7, %14, %6\n\t"
-        "v_mad_u64_u32 %0, vcc, %8, %15, %0\n\t"
-        "v_mad_u64_u32 %1, vcc, %8, %16, %1\n\t"
-        "v_mad_u64_u32 %2, vcc, %8, %17, %2\n\t"
-        "v_mad_u64_u32 %3, vcc, %8, %18, %3\n\t"
-        "v_mad_u64_u32 %4, vcc, %8, %19, %4\n\t"
-        "v_mad_u64_u32 %5, vcc, %8, %20, %5"
-        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4])
-        : "v"(T[j + 5]), "v"(e), "v"(m), "v"(a[j]), "v"(a[j + 1]), "v"(a[j + 2]), "v"(a[j + 3]), "v"(a[j + 4]),
-          "v"(a[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]), "s"(p[j + 4]), "s"(p[j + 5])
-        : "vcc");
-  }
-  // T2[j-1+k] = T2[j+k] + e c[j+k] + f a[j+k] + m P[j+k], k = 0..5
-  XHE_DEV void blk2(uint64_t (&T)[K], const uint32_t (&c)[K], const uint32_t (&a)[K], uint32_t e, uint32_t f,
-                    uint32_t m, int j) const {
-    asm("v_mad_u64_u32 %0, vcc, %7, %10, %1\n\t"
-        "v_mad_u64_u32 %1, vcc, %7, %11, %2\n\t"
-        "v_mad_u64_u32 %2, vcc, %7, %12, %3\n\t"
-        "v_mad_u64_u32 %3, vcc, %7, %13, %4\n\t"
-        "v_mad_u64_u32 %4, vcc, %7, %14, %5\n\t"
-        "v_mad_u64_u32 %5, vcc, %7, %15, %6\n\t"
-        "v_mad_u64_u32 %0, vcc, %8, %16, %0\n\t"
-        "v_mad_u64_u32 %1, vcc, %8, %17, %1\n\t"
-        "v_mad_u64_u32 %2, vcc, %8, %18, %2\n\t"
-        "v_mad_u64_u32 %3, vcc, %8, %19, %3\n\t"
-        "v_mad_u64_u32 %4, vcc, %8, %20, %4\n\t"
-        "v_mad_u64_u32 %5, vcc, %8, %21, %5\n\t"
-        "v_mad_u64_u32 %0, vcc, %9, %22, %0\n\t"
-        "v_mad_u64_u32 %1, vcc, %9, %23, %1\n\t"
-        "v_mad_u64_u32 %2, vcc, %9, %24, %2\n\t"
-        "v_mad_u64_u32 %3, vcc, %9, %25, %3\n\t"
-        "v_mad_u64_u32 %4, vcc, %9, %26, %4\n\t"
-        "v_mad_u64_u32 %5, vcc, %9, %27, %5"
-        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4])
-        : "v"(T[j + 5]), "v"(e), "v"(f), "v"(m), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]), "v"(c[j + 3]),
-          "v"(c[j + 4]), "v"(c[j + 5]), "v"(a[j]), "v"(a[j + 1]), "v"(a[j + 2]), "v"(a[j + 3]), "v"(a[j + 4]),
-          "v"(a[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]), "s"(p[j + 4]), "s"(p[j + 5])
-        : "vcc");
-  }
-
-  // squaring form of blk2: T2[j-1+k] = T2[j+k] + e2 c[j+k] + m P[j+k] (e2 = 2 a_i)
-  XHE_DEV void blk2s(uint64_t (&T)[K], const uint32_t (&c)[K], uint32_t e2, uint32_t m, int j) const {
-    asm("v_mad_u64_u32 %0, vcc, %7, %9, %1\n\t"
-        "v_mad_u64_u32 %1, vcc, %7, %10, %2\n\t"
-        "v_mad_u64_u32 %2, vcc, %7, %11, %3\n\t"
-        "v_mad_u64_u32 %3, vcc, %7, %12, %4\n\t"
-        "v_mad_u64_u32 %4, vcc, %7, %13, %5\n\t"
-        "v_mad_u64_u32 %5, vcc, %7, %14, %6\n\t"
-        "v_mad_u64_u32 %0, vcc, %8, %15, %0\n\t"
-        "v_mad_u64_u32 %1, vcc, %8, %16, %1\n\t"
-        "v_mad_u64_u32 %2, vcc, %8, %17, %2\n\t"
-        "v_mad_u64_u32 %3, vcc, %8, %18, %3\n\t"
-        "v_mad_u64_u32 %4, vcc, %8, %19, %4\n\t"
-        "v_mad_u64_u32 %5, vcc, %8, %20, %5"
-        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4])
-        : "v"(T[j + 5]), "v"(e2), "v"(m), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]), "v"(c[j + 3]), "v"(c[j + 4]),
-          "v"(c[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]), "s"(p[j + 4]), "s"(p[j + 5])
-        : "vcc");
+  // One block of 6 positions of both accumulators in ONE asm statement (tied
+  // accumulators: T[j-1+k] is written after its old value was consumed, so
+  // the registers stay put and no rotation copies appear; the compiler puts
+  // a hazard nop after every asm statement, so one statement per block):
+  //   T1[j-1+k] = T1[j+k] + e a[j+k] + m1 P[j+k]
+  //   T2[j-1+k] = T2[j+k] + e c[j+k] + f a[j+k] + m2 P[j+k]   (SQ: f (= 2 a_i) c[j+k] + m2 P[j+k])
+  template <bool SQ>
+  XHE_DEV void blk12(uint64_t (&T1)[K], uint64_t (&T2)[K], const uint32_t (&a)[K], const uint32_t (&c)[K],
+                     uint32_t e, uint32_t f, uint32_t m1, uint32_t m2, int j) const {
+    if constexpr (SQ) {
+      asm(
+        "v_mad_u64_u32 %0, vcc, %14, %18, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %14, %19, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %14, %20, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %14, %21, %4\n\t"
+        "v_mad_u64_u32 %4, vcc, %14, %22, %5\n\t"
+        "v_mad_u64_u32 %5, vcc, %14, %23, %12\n\t"
+        "v_mad_u64_u32 %6, vcc, %15, %24, %7\n\t"
+        "v_mad_u64_u32 %7, vcc, %15, %25, %8\n\t"
+        "v_mad_u64_u32 %8, vcc, %15, %26, %9\n\t"
+        "v_mad_u64_u32 %9, vcc, %15, %27, %10\n\t"
+        "v_mad_u64_u32 %10, vcc, %15, %28, %11\n\t"
+        "v_mad_u64_u32 %11, vcc, %15, %29, %13\n\t"
+        "v_mad_u64_u32 %0, vcc, %16, %30, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %16, %31, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %16, %32, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %16, %33, %3\n\t"
+        "v_mad_u64_u32 %4, vcc, %16, %34, %4\n\t"
+        "v_mad_u64_u32 %5, vcc, %16, %35, %5\n\t"
+        "v_mad_u64_u32 %6, vcc, %17, %30, %6\n\t"
+        "v_mad_u64_u32 %7, vcc, %17, %31, %7\n\t"
+        "v_mad_u64_u32 %8, vcc, %17, %32, %8\n\t"
+        "v_mad_u64_u32 %9, vcc, %17, %33, %9\n\t"
+        "v_mad_u64_u32 %10, vcc, %17, %34, %10\n\t"
+        "v_mad_u64_u32 %11, vcc, %17, %35, %11"
+          : "+v"(T1[j - 1]), "+v"(T1[j]), "+v"(T1[j + 1]), "+v"(T1[j + 2]), "+v"(T1[j + 3]), "+v"(T1[j + 4]),
+            "+v"(T2[j - 1]), "+v"(T2[j]), "+v"(T2[j + 1]), "+v"(T2[j + 2]), "+v"(T2[j + 3]), "+v"(T2[j + 4])
+          : "v"(T1[j + 5]), "v"(T2[j + 5]), "v"(e), "v"(f), "v"(m1), "v"(m2), "v"(a[j]), "v"(a[j + 1]),
+            "v"(a[j + 2]), "v"(a[j + 3]), "v"(a[j + 4]), "v"(a[j + 5]), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]),
+            "v"(c[j + 3]), "v"(c[j + 4]), "v"(c[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]),
+            "s"(p[j + 4]), "s"(p[j + 5])
+          : "vcc");
+    } else {
+      asm(
+        "v_mad_u64_u32 %0, vcc, %14, %18, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %14, %19, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %14, %20, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %14, %21, %4\n\t"
+        "v_mad_u64_u32 %4, vcc, %14, %22, %5\n\t"
+        "v_mad_u64_u32 %5, vcc, %14, %23, %12\n\t"
+        "v_mad_u64_u32 %6, vcc, %14, %24, %7\n\t"
+        "v_mad_u64_u32 %7, vcc, %14, %25, %8\n\t"
+        "v_mad_u64_u32 %8, vcc, %14, %26, %9\n\t"
+        "v_mad_u64_u32 %9, vcc, %14, %27, %10\n\t"
+        "v_mad_u64_u32 %10, vcc, %14, %28, %11\n\t"
+        "v_mad_u64_u32 %11, vcc, %14, %29, %13\n\t"
+        "v_mad_u64_u32 %0, vcc, %16, %30, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %16, %31, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %16, %32, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %16, %33, %3\n\t"
+        "v_mad_u64_u32 %4, vcc, %16, %34, %4\n\t"
+        "v_mad_u64_u32 %5, vcc, %16, %35, %5\n\t"
+        "v_mad_u64_u32 %6, vcc, %15, %18, %6\n\t"
+        "v_mad_u64_u32 %7, vcc, %15, %19, %7\n\t"
+        "v_mad_u64_u32 %8, vcc, %15, %20, %8\n\t"
+        "v_mad_u64_u32 %9, vcc, %15, %21, %9\n\t"
+        "v_mad_u64_u32 %10, vcc, %15, %22, %10\n\t"
+        "v_mad_u64_u32 %11, vcc, %15, %23, %11\n\t"
+        "v_mad_u64_u32 %6, vcc, %17, %30, %6\n\t"
+        "v_mad_u64_u32 %7, vcc, %17, %31, %7\n\t"
+        "v_mad_u64_u32 %8, vcc, %17, %32, %8\n\t"
+        "v_mad_u64_u32 %9, vcc, %17, %33, %9\n\t"
+        "v_mad_u64_u32 %10, vcc, %17, %34, %10\n\t"
+        "v_mad_u64_u32 %11, vcc, %17, %35, %11"
+          : "+v"(T1[j - 1]), "+v"(T1[j]), "+v"(T1[j + 1]), "+v"(T1[j + 2]), "+v"(T1[j + 3]), "+v"(T1[j + 4]),
+            "+v"(T2[j - 1]), "+v"(T2[j]), "+v"(T2[j + 1]), "+v"(T2[j + 2]), "+v"(T2[j + 3]), "+v"(T2[j + 4])
+          : "v"(T1[j + 5]), "v"(T2[j + 5]), "v"(e), "v"(f), "v"(m1), "v"(m2), "v"(a[j]), "v"(a[j + 1]),
+            "v"(a[j + 2]), "v"(a[j + 3]), "v"(a[j + 4]), "v"(a[j + 5]), "v"(c[j]), "v"(c[j + 1]), "v"(c[j + 2]),
+            "v"(c[j + 3]), "v"(c[j + 4]), "v"(c[j + 5]), "s"(p[j]), "s"(p[j + 1]), "s"(p[j + 2]), "s"(p[j + 3]),
+            "s"(p[j + 4]), "s"(p[j + 5])
+          : "vcc");
+    }
   }
 
   // One step of the two interleaved reductions on row limbs (e, f). Entry:
@@ -133,22 +149,34 @@ struct PMD {
                     uint64_t& x2, uint32_t topc) const {
     uint64_t x1n = 0, x2n = 0;
     uint32_t t1 = 0, t2 = 0, m1n = 0, m2n = 0;
-    x1 = mad64s(m1, p[0], x1);  // now = 0 (mod 2^W)
-    x2 = mad64s(m2, p[0], x2);
+    asm("v_mad_u64_u32 %0, vcc, %2, %4, %0\n\t"  // x1 += m1 P_0: now = 0 (mod 2^W); x2 likewise
+        "v_mad_u64_u32 %1, vcc, %3, %4, %1"
+        : "+v"(x1), "+v"(x2)
+        : "v"(m1), "v"(m2), "s"(p[0])
+        : "vcc");
 #pragma unroll
     for (int b = 0; b < (K - 1) / BL; ++b) {
       const int j = 1 + BL * b;
-      blk1(T1, a, e, m1, j);
-      if constexpr (SQ) blk2s(T2, c, e << 1, m2, j);
-      else blk2(T2, c, a, e, f, m2, j);
+      blk12<SQ>(T1, T2, a, c, e, SQ ? (e << 1) : f, m1, m2, j);
       if (b == 0) {
         T1[0] += x1 >> W;
         T2[0] += x2 >> W;
         asm volatile("" : "+v"(T1[0]), "+v"(T2[0]));
       } else if (b == 1) {
-        x1n = mad64(en, a[0], T1[0]);
-        if constexpr (SQ) x2n = mad64(en << 1, c[0], T2[0]);
-        else x2n = mad64(fn, a[0], mad64(en, c[0], T2[0]));
+        if constexpr (SQ) {
+          asm("v_mad_u64_u32 %0, vcc, %2, %3, %5\n\t"
+              "v_mad_u64_u32 %1, vcc, %4, %7, %6"
+              : "=&v"(x1n), "=v"(x2n)
+              : "v"(en), "v"(a[0]), "v"(en << 1), "v"(T1[0]), "v"(T2[0]), "v"(c[0])
+              : "vcc");
+        } else {
+          asm("v_mad_u64_u32 %0, vcc, %2, %4, %6\n\t"
+              "v_mad_u64_u32 %1, vcc, %2, %5, %7\n\t"
+              "v_mad_u64_u32 %1, vcc, %3, %4, %1"
+              : "=&v"(x1n), "=&v"(x2n)
+              : "v"(en), "v"(fn), "v"(a[0]), "v"(c[0]), "v"(T1[0]), "v"(T2[0])
+              : "vcc");
+        }
         asm volatile("" : "+v"(x1n), "+v"(x2n));
       } else if (b == 2) {
         t1 = (uint32_t)x1n * n0inv;
