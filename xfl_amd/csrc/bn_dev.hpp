@@ -71,6 +71,32 @@ XHE_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "vcc");
   return c;
 }
+// T[j-1] = T[j] + a b[j] for j = 1..N-1 (the shift of an operand-scanning
+// row), six positions per asm statement: tied accumulators (T[j-1] is
+// written after its old value was consumed, no rotation copies), and the
+// compiler puts a hazard nop after every asm statement, not inside one
+template <int N>
+XHE_DEV void mad_shift(uint64_t (&T)[N], const uint32_t (&b)[N], uint32_t a) {
+  int j = 1;
+#pragma unroll
+  for (; j + 6 <= N; j += 6)
+    asm("v_mad_u64_u32 %0, vcc, %7, %8, %1\n\t"
+        "v_mad_u64_u32 %1, vcc, %7, %9, %2\n\t"
+        "v_mad_u64_u32 %2, vcc, %7, %10, %3\n\t"
+        "v_mad_u64_u32 %3, vcc, %7, %11, %4\n\t"
+        "v_mad_u64_u32 %4, vcc, %7, %12, %5\n\t"
+        "v_mad_u64_u32 %5, vcc, %7, %13, %6"
+        : "+v"(T[j - 1]), "+v"(T[j]), "+v"(T[j + 1]), "+v"(T[j + 2]), "+v"(T[j + 3]), "+v"(T[j + 4])
+        : "v"(T[j + 5]), "v"(a), "v"(b[j]), "v"(b[j + 1]), "v"(b[j + 2]), "v"(b[j + 3]), "v"(b[j + 4]),
+          "v"(b[j + 5])
+        : "vcc");
+#pragma unroll
+  for (; j < N; ++j) {
+    uint64_t t = T[j];
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(t) : "v"(a), "v"(b[j]) : "vcc");
+    T[j - 1] = t;
+  }
+}
 // same with a wave-uniform b (SGPR operand)
 XHE_DEV uint64_t mad64s(uint32_t a, uint32_t b_uniform, uint64_t c) {
   asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "s"(b_uniform) : "vcc");
@@ -980,8 +1006,7 @@ struct Mont {
           uint32_t ai = comp4(a4, r);
           uint64_t x0 = mad64(ai, b[0], T[0]);
           if (lead) ws[(size_t)(i0 + r) * stride] = (uint32_t)x0 & MASK;
-#pragma unroll
-          for (int j = 1; j < L; ++j) T[j - 1] = mad64(ai, b[j], T[j]);
+          mad_shift(T, b, ai);
           T[L - 1] = G::from_next64(x0);
           T[0] += lead ? (x0 >> W) : 0ull;
         }

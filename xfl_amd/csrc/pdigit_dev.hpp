@@ -798,8 +798,7 @@ struct PMDX {
         const uint32_t m = G::bcast0(((uint32_t)T[0] * M.n0inv) & MASK);
         mq[jj] = g == ib ? m : mq[jj];
         const uint64_t v = mad64(m, M.nl[0], T[0]);
-#pragma unroll
-        for (int j = 1; j < L; ++j) T[j - 1] = mad64(m, M.nl[j], T[j]);
+        mad_shift(T, M.nl, m);
         T[0] += v >> W;
         const uint32_t d = G::from_next((uint32_t)v & MASK);
         const uint32_t h = HI ? from_lane_i(xh[jj], ib) : 0u;

@@ -1493,8 +1493,7 @@ __global__ void __launch_bounds__(256, 2) k_crt_enc_w(KeyDev key, const uint32_t
       if (i0 + r < S) {
         const uint32_t ai = comp4(a4, r);
         const uint64_t x0 = mad64(ai, b[0], T[0]);
-#pragma unroll
-        for (int j = 1; j < S; ++j) T[j - 1] = mad64(ai, b[j], T[j]);
+        mad_shift(T, b, ai);
         T[S - 1] = 0;
         T[0] += x0 >> W;
         emit((uint32_t)x0 & MP2::MASK);
@@ -1703,8 +1702,7 @@ __global__ void __launch_bounds__(256, 2) k_dec_fin(KeyDev key, const uint32_t* 
           uint32_t ai = comp4(a4, r);
           uint64_t x0 = mad64(ai, q[0], T[0]);
           if (lead) mrow[(size_t)(i0 + r) * st] = (uint32_t)x0 & MP::MASK;
-#pragma unroll
-          for (int j = 1; j < MP::L; ++j) T[j - 1] = mad64(ai, q[j], T[j]);
+          mad_shift(T, q, ai);
           T[MP::L - 1] = MP::G::from_next64(x0);
           T[0] += lead ? (x0 >> MP::W) : 0ull;
         }
