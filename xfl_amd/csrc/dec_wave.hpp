@@ -33,14 +33,6 @@
 
 namespace xhe {
 
-#ifndef XHE_WAVE_FUSED
-// 1: the normalisations fused into the next product's operand reads (4 LDS
-// phases per product instead of 6). Measured slower (k_dec_wave 2.23 -> 3.22
-// ms for 15 elements under rocprof): every thread of a slice recomputes the
-// slice's 16 limbs from 3 x 18 column reads (37x redundant LDS traffic), more
-// than the sync it saves. Kept as an A/B switch.
-#define XHE_WAVE_FUSED 0
-#endif
 #ifndef XHE_WAVE_PROF
 #define XHE_WAVE_PROF 0  // dev builds: cycles per phase of block (0, 0), printed at the end
 #endif
@@ -132,35 +124,17 @@ struct WaveMont {
   // (consecutive term quads share one), 4 TS mads into four accumulators
   // (one per column), then one LDS atomic per column. LO: columns < K + 2
   // only (the quotient product; its columns from K on are never read).
-  // FUSED: the multiplier is norm() of the lazy columns acg (= col + G)
-  // below limb K, formed by each thread for its own slice of terms straight
-  // from the columns (no normalisation phase and no sync before the
-  // product); else the limbs a. ZERO: the idle threads zero the other
-  // column buffer (last read by the previous product's tail, next written
-  // by the next product).
-  template <bool LO, bool FUSED = false>
-  static XHE_DEV void prodq(const uint32_t* a, const uint64_t* acg, const uint32_t* z, uint64_t* col,
-                            uint64_t* zero = nullptr) {
+  // ZERO: the idle threads zero the other column buffer (last read by the
+  // previous product's tail, next written by the next product).
+  template <bool LO>
+  static XHE_DEV void prodq(const uint32_t* a, const uint32_t* z, uint64_t* col, uint64_t* zero = nullptr) {
     constexpr int NQ = LO ? NQL : NQF;
     const int q = tid() % NQ, sl = tid() / NQ;
     if (sl < NS) {
       const int t0 = sl * TS;
       uint4 av[TS / 4], zq[TS / 4 + 1];
-      if constexpr (FUSED) {
-        // split3 of columns t0-1 .. t0+TS-1 (reads columns t0-3 .. t0+TS-1;
-        // the G guards below column 0 are zero), then the second pass
-        uint32_t s3[TS + 1];
 #pragma unroll
-        for (int k = 0; k <= TS; ++k) s3[k] = t0 - 1 + k < K ? split3(acg, t0 - 1 + k) : 0u;  // (mcol ends at 4 NQL)
-        uint32_t v[TS];
-#pragma unroll
-        for (int k = 0; k < TS; ++k) v[k] = t0 + k < K ? (s3[k + 1] & MASK) + (s3[k] >> W) : 0u;
-#pragma unroll
-        for (int u = 0; u < TS / 4; ++u) av[u] = make_uint4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
-      } else {
-#pragma unroll
-        for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
-      }
+      for (int u = 0; u < TS / 4; ++u) av[u] = *reinterpret_cast<const uint4*>(a + t0 + 4 * u);
       // quad u of terms needs Z[B_u - 4 .. B_u + 3], B_u = ZO + 4q - t0 - 4u:
       // zq[u + 1] = Z[B_u - 4 ..], zq[u] = Z[B_u ..]
       const uint32_t* zb0 = z + (ZO + 4 * q - t0);
@@ -226,24 +200,16 @@ struct WaveMont {
     sync();
   }
 
-  // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N). Three
-  // phases: the quotient product reads T mod R straight from the columns,
-  // the U product reads m from its columns (round 4; the separate
-  // normalisation phases before each took 6 phases per product to 4).
+  // dst = REDC(T), T in s.col[cur] (< R N): T R^-1 mod N (< 2N): T's low
+  // limbs, the quotient product m = (T mod R) N' mod R, m's limbs, the U
+  // product, the tail (five LDS phases after T's own)
   static XHE_DEV void reduce(Lds& s, int cur, uint32_t* dst, bool zbw) {
-#if XHE_WAVE_FUSED
-    prodq<true, true>(nullptr, s.col[cur] + G, s.znp, s.mcol, s.col[cur ^ 1]);  // m = (T mod R) N' mod R
-    XHE_WAVE_T(1);
-    prodq<false, true>(nullptr, s.mcol + G, s.zn, s.col[cur]);  // U = T + m N
-    XHE_WAVE_T(2);
-#else
     norm_low_t(s, cur);
-    prodq<true>(s.tl, nullptr, s.znp, s.mcol);  // m = (T mod R) N' mod R
+    prodq<true>(s.tl, s.znp, s.mcol);  // m = (T mod R) N' mod R
     XHE_WAVE_T(1);
     norm_low(s.mcol, s.mq);
-    prodq<false>(s.mq, nullptr, s.zn, s.col[cur]);  // U = T + m N
+    prodq<false>(s.mq, s.zn, s.col[cur]);  // U = T + m N
     XHE_WAVE_T(2);
-#endif
     tail(s, cur, dst, zbw);
     XHE_WAVE_T(3);
   }
@@ -253,7 +219,7 @@ struct WaveMont {
   static XHE_DEV void mul(Lds& s, int& cur, const uint32_t* a, uint32_t* dst, bool zbw) {
     cur ^= 1;
     XHE_WAVE_T(-1);
-    prodq<false>(a, nullptr, s.zb, s.col[cur]);
+    prodq<false>(a, s.zb, s.col[cur]);
     XHE_WAVE_T(0);
     reduce(s, cur, dst, zbw);
   }
