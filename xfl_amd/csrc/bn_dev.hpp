@@ -43,12 +43,6 @@ namespace xhe {
 #ifndef XHE_DJN_FOLD
 #define XHE_DJN_FOLD 1  // k_djn_pow_lds: (1 + n m) as the last (plain) multiplier, nwin + 1 products
 #endif
-#ifndef XHE_M_MAD
-#define XHE_M_MAD 0  // Montgomery digit m = x0 * n0inv by v_mad_u64_u32 instead of v_mul_lo_u32
-#endif
-#ifndef XHE_PQ_PAIR
-#define XHE_PQ_PAIR 0  // 1: DJN tables with p^2/q^2 rows of one (window, digit) adjacent and k_djn_pow_lds pairing p/q blocks per XCD (A/B: no gain)
-#endif
 #ifndef XHE_SQ_ACC
 #define XHE_SQ_ACC 2  // partial sums per column of Mont::sqr's product scan
 #endif
@@ -60,9 +54,6 @@ namespace xhe {
 #endif
 #ifndef XHE_NDIG
 #define XHE_NDIG 1  // 2048-bit n^2 exponentiations (public non-DJN r^n, scalar mul c^k) in Montgomery digits mod n^2
-#endif
-#ifndef XHE_APREF2
-#define XHE_APREF2 0  // TPI==1: operand a loaded two quads (8 columns) ahead
 #endif
 // d = a*b + c with one v_mad_u64_u32. Inline asm keeps a and b 32-bit: the
 // C form (uint64_t)a*b + c makes the compiler hold every limb as a
@@ -712,11 +703,7 @@ struct Mont {
         xn = mad64(ai_next, b[0], T[0]);
         asm volatile("" : "+v"(xn));
       } else if (stage == 2) {
-#if XHE_M_MAD
-        t = (uint32_t)mad64((uint32_t)xn, n0inv, 0ull);
-#else
         t = (uint32_t)xn * n0inv;
-#endif
         asm volatile("" : "+v"(t));
       } else if (stage == 3) {
         mn = G::bcast0(t & MASK);
@@ -828,24 +815,6 @@ struct Mont {
     if constexpr (TPI == 1 && L >= 13) {
       NRes R;
       load_res(Np, R);
-#if XHE_APREF2
-      // operand a two quads ahead (a gathered table row misses L2 often)
-      uint4 nx1 = a.load4(4 < S4 ? 4 : 0);
-      for (; i + 4 <= S; i += 4) {
-        uint4 nx2 = a.load4(i + 8 < S4 ? i + 8 : i);
-        __builtin_amdgcn_sched_barrier(0);
-        step1(Np, R, T, b, cur.x, cur.y, m, x0, lead);
-        __builtin_amdgcn_sched_barrier(0);
-        step1(Np, R, T, b, cur.y, cur.z, m, x0, lead);
-        __builtin_amdgcn_sched_barrier(0);
-        step1(Np, R, T, b, cur.z, cur.w, m, x0, lead);
-        __builtin_amdgcn_sched_barrier(0);
-        step1(Np, R, T, b, cur.w, nx1.x, m, x0, lead);
-        __builtin_amdgcn_sched_barrier(0);
-        cur = nx1;
-        nx1 = nx2;
-      }
-#else
       for (; i + 4 <= S; i += 4) {
         uint4 nxt = a.load4(i + 4 < S4 ? i + 4 : i);
         __builtin_amdgcn_sched_barrier(0);
@@ -859,7 +828,6 @@ struct Mont {
         __builtin_amdgcn_sched_barrier(0);
         cur = nxt;
       }
-#endif
 #pragma unroll
       for (int r = 0; r < (S & 3); ++r)
         step1(Np, R, T, b, comp4(cur, r), r + 1 < (S & 3) ? comp4(cur, r + 1) : 0u, m, x0, lead);

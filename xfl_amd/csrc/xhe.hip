@@ -682,15 +682,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       size_t rows = (size_t)(kd.nwin + kd.nhi) << kd.win;
       size_t tab_words = rows * (size_t)(K / 32);  // packed rows: Shape::RW = K/32 words (p^2 < 2^K)
       HIPCHK(hipMalloc(&k->d_tab, 2 * tab_words * sizeof(uint32_t)));
-#if XHE_PQ_PAIR
-      kd.tab_rs = 2 * (K / 32);  // rows (w, d) of p^2 and q^2 side by side
-      kd.tab_p2 = k->d_tab;
-      kd.tab_q2 = k->d_tab + K / 32;
-#else
       kd.tab_rs = K / 32;
       kd.tab_p2 = k->d_tab;
       kd.tab_q2 = k->d_tab + tab_words;
-#endif
       const ModDev mds[2] = {kd.p2, kd.q2};
       const uint32_t* hms[2] = {B + o.hM_p2, B + o.hM_q2};
       uint32_t* tabs[2] = {const_cast<uint32_t*>(kd.tab_p2), const_cast<uint32_t*>(kd.tab_q2)};
@@ -961,11 +955,7 @@ void encrypt_impl(const xhe_key* k, const uint32_t* m, const uint32_t* r, int64_
       ProfScope ps(XHE_LDS_ROWS && MP2::TPI == 1 ? "k_djn_pow_lds" : "k_djn_pow", s);
 #if XHE_LDS_ROWS
       if constexpr (MP2::TPI == 1) {
-#if XHE_PQ_PAIR
-        const dim3 grid((unsigned)(16 * ((n + 1023) / 1024)));  // 8 chunks of 128 elements x 2 primes per 16 blocks
-#else
         const dim3 grid((unsigned)((n + 127) / 128), 2);
-#endif
         hipLaunchKernelGGL((k_djn_pow_lds<MP2, Sh::RW>), grid, dim3(128), 0, s, k->kd,
                            k->kd.p2.N, k->kd.q2.N, m + (size_t)off * k->nw, r + (size_t)off * k->rand_words,
                            k->rand_words, n, ws);

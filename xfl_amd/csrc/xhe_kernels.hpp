@@ -63,7 +63,7 @@ struct KeyDev {
   const uint32_t* q2_lim;     // q^2 (MP2 limbs)
   const uint32_t* p2x4_lim;   // 4 p^2 (MP2 limbs)
   const uint32_t* tab_p2;     // h^(d*2^bit(w)) * R mod p^2, packed rows, windows as win_digit()
-  const uint32_t* tab_q2;     // (XHE_PQ_PAIR: interleaved with tab_p2, row (w, d) of q^2 right after p^2's)
+  const uint32_t* tab_q2;
   int64_t tab_rs;             // words from one row of tab_p2 / tab_q2 to the next
   int win, nwin, nhi;         // nhi: the first nhi windows are win+1 bits wide (0: uniform)
   // ---- mod p / q (shape MP), decrypt
@@ -606,20 +606,8 @@ __global__ void __launch_bounds__(128, 2) k_djn_pow_lds(KeyDev key, const uint32
                                                         uint32_t* __restrict__ ws) {
   static_assert(MP2::TPI == 1, "LDS row staging is per lane");
   __shared__ __attribute__((aligned(16))) uint32_t img_all[2][(MP2::S4 / 4) * 256];
-#if XHE_PQ_PAIR
-  // 1-D grid: block b runs on XCD b % 8 (round-robin dispatch; for speed
-  // only, correctness does not depend on it); of each XCD's consecutive
-  // blocks, two take the same element block for p^2 and q^2, so both read
-  // the same (window, digit) row pair - one TLB entry and one DRAM page -
-  // at about the same time on the same L2.
-  const int64_t bid = blockIdx.x, j = bid >> 3;
-  const int prime = (int)(j & 1);
-  const int64_t chunk = ((j >> 1) << 3) | (bid & 7);
-  const int64_t e = chunk * blockDim.x + threadIdx.x;
-#else
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int prime = blockIdx.y;
-#endif
   uint32_t* img = img_all[(threadIdx.x >> 6) & 1];
   if (e >= count) return;
   djn_prime_lds<MP2, RW>(key, prime ? Nq2 : Np2, prime ? key.q2 : key.p2, prime ? key.tab_q2 : key.tab_p2,
