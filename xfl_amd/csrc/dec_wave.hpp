@@ -97,16 +97,29 @@ struct WaveMont {
   static XHE_DEV int tid() { return (int)threadIdx.x; }
   static XHE_DEV void sync() { __syncthreads(); }
 
-  // acc[k] += a_k b_k, k = 0..3: four independent accumulators in one asm
-  // statement (no dependent mads back to back, no hazard nops between them)
-  static XHE_DEV void mad4(uint64_t (&acc)[4], uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0,
-                           uint32_t b1, uint32_t b2, uint32_t b3) {
-    asm("v_mad_u64_u32 %0, vcc, %4, %8, %0\n\t"
-        "v_mad_u64_u32 %1, vcc, %5, %9, %1\n\t"
-        "v_mad_u64_u32 %2, vcc, %6, %10, %2\n\t"
-        "v_mad_u64_u32 %3, vcc, %7, %11, %3"
+  // acc[i] += a_r z[4 + i - r] for r, i < 4: one term quad of a column quad,
+  // 16 mads in one statement (a hazard nop follows every asm statement; the
+  // same accumulator recurs every 4 mads)
+  static XHE_DEV void mad16(uint64_t (&acc)[4], const uint32_t (&a)[4], const uint32_t (&z)[8]) {
+    asm("v_mad_u64_u32 %0, vcc, %4, %12, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %4, %13, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %4, %14, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %4, %15, %3\n\t"
+        "v_mad_u64_u32 %0, vcc, %5, %11, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %5, %12, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %5, %13, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %5, %14, %3\n\t"
+        "v_mad_u64_u32 %0, vcc, %6, %10, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %6, %11, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %6, %12, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %6, %13, %3\n\t"
+        "v_mad_u64_u32 %0, vcc, %7, %9, %0\n\t"
+        "v_mad_u64_u32 %1, vcc, %7, %10, %1\n\t"
+        "v_mad_u64_u32 %2, vcc, %7, %11, %2\n\t"
+        "v_mad_u64_u32 %3, vcc, %7, %12, %3"
         : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
-        : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]), "v"(z[4]),
+          "v"(z[5]), "v"(z[6]), "v"(z[7])
         : "vcc");
   }
 
@@ -140,18 +153,19 @@ struct WaveMont {
       const uint32_t* zb0 = z + (ZO + 4 * q - t0);
 #pragma unroll
       for (int u = 0; u <= TS / 4; ++u) zq[u] = *reinterpret_cast<const uint4*>(zb0 - 4 * u);
-      uint64_t acc[4] = {0ull, 0ull, 0ull, 0ull};
+      // two accumulator sets (term quads alternate), so one quad's mads do
+      // not wait on the previous quad's
+      uint64_t acc[2][4] = {{0ull, 0ull, 0ull, 0ull}, {0ull, 0ull, 0ull, 0ull}};
 #pragma unroll
       for (int u = 0; u < TS / 4; ++u) {
         const uint32_t zz[8] = {zq[u + 1].x, zq[u + 1].y, zq[u + 1].z, zq[u + 1].w,
                                 zq[u].x,     zq[u].y,     zq[u].z,     zq[u].w};  // Z[B_u - 4 + k]
         const uint32_t at[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)  // column 4q + i, term t0 + 4u + r: Z[B_u + i - r]
-          mad4(acc, at[r], at[r], at[r], at[r], zz[4 - r], zz[5 - r], zz[6 - r], zz[7 - r]);
+        mad16(acc[u & 1], at, zz);  // column 4q + i, term t0 + 4u + r: Z[B_u + i - r]
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long*)&col[G + 4 * q + i], (unsigned long long)acc[i]);
+      for (int i = 0; i < 4; ++i)
+        atomicAdd((unsigned long long*)&col[G + 4 * q + i], (unsigned long long)(acc[0][i] + acc[1][i]));
     } else if (zero) {
       for (int i = tid() - NQ * NS; i < 2 * K; i += NT - NQ * NS) zero[G + i] = 0ull;
     }
