@@ -339,6 +339,7 @@ def measure_dropin(nat, device, key_bits, xh, key_material):
     out["dropin_chain_max_abs_err"] = float(np.max(np.abs(got - r.astype(np.float64) @ X)))
     note("dropin_chain_encrypt_matmul_serialize_2048x15_s")
     out["dropin_table_bytes_w16"] = nat.table_bytes(key_bits, 16)
+    out.update(measure_dropin_histogram(ctx))
     # the policy's steady state for a loop of 1 M-element calls: past 64 M
     # encrypted elements the key's tables are rebuilt at window 22 (when they
     # leave 32 GiB free; the rebuild happens in the untimed first call)
@@ -357,6 +358,72 @@ def measure_dropin(nat, device, key_bits, xh, key_material):
     ctx._dev = {}
     gc.collect()
     torch.cuda.empty_cache()
+    return out
+
+
+def xgb_inputs(n=100_000, nfeat=64, nbins=256):
+    """BASELINE config 5's synthetic inputs: g = sigmoid(z) - y,
+    h = p (1 - p) (seed 3), bins ~ U{0..255} per feature (seed 4 + f)"""
+    import pandas as pd
+    rng = np.random.default_rng(3)
+    p = 1 / (1 + np.exp(-rng.standard_normal(n)))
+    y = rng.integers(0, 2, n)
+    g, h = p - y, p * (1 - p)
+    values = pd.DataFrame({f"x{f}": np.random.default_rng(4 + f).integers(0, nbins, n).astype(np.uint8)
+                           for f in range(nfeat)})
+    return g, h, values
+
+
+def measure_dropin_histogram(ctx, n=100_000, nfeat=64):
+    """Config 5 through XFL's own pandas calls: the label side's embed ->
+    Paillier.encrypt(precision=0) -> serialize(compression=False), the
+    trainer's ciphertext_from -> Feature.create (core/tree/big_feature.py:
+    43-46) -> per feature groupby(col)['xfl_grad_hess'].agg({'count', 'sum'})
+    (xgboost/decision_tree_trainer.py:151-152) -> res_hist['sum'].to_numpy()
+    (:180). Timed: the 64 groupby calls with every bin sum computed (host
+    pandas work included), and the same with the operator's to_numpy."""
+    import pandas as pd
+    import torch
+    from xfl_amd.paillier import Paillier
+    from xfl_amd.paillier.array import PaillierDtype
+    from xfl_amd.paillier_acceleration import embed
+    g, h, values = xgb_inputs(n, nfeat)
+    enc = Paillier.encrypt(ctx, embed([g, h], interval=1 << 128, precision=64), precision=0)
+    wire = Paillier.serialize(enc, compression=False)
+    del enc
+    grad_hess = Paillier.ciphertext_from(ctx.to_public(), wire, compression=False)
+    data = pd.concat([pd.DataFrame(range(n), columns=['xfl_id']), pd.DataFrame(grad_hess, columns=['xfl_grad_hess']),
+                      values], axis=1)
+    out = {"dropin_groupby_column_dtype": str(data['xfl_grad_hess'].dtype)}
+    cols = list(values.columns)
+
+    def hist(to_numpy):
+        res = [data.groupby([c])['xfl_grad_hess'].agg({'count', 'sum'}) for c in cols]
+        if to_numpy:
+            return [(r['sum'].to_numpy(), r['count'].to_numpy()) for r in res]
+        for r in res:
+            if isinstance(r['sum'].dtype, PaillierDtype):
+                r['sum'].values.is_resident  # noqa: B018 (results computed: the sync below waits for them)
+        torch.cuda.synchronize()
+        return res
+    hist(False)  # first call uploads the column's words once (the later calls read them in HBM)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    res = hist(False)
+    out[f"dropin_groupby_100k_x{nfeat}_s"] = time.time() - t0
+    t0 = time.time()
+    hist(True)
+    out[f"dropin_groupby_100k_x{nfeat}_to_numpy_s"] = time.time() - t0
+    # check: decrypted bins of 2 features = the exact integer sums of the embedded values
+    from xfl_amd.paillier_acceleration import embed as emb
+    ints = emb([g, h], interval=1 << 128, precision=64)
+    ok = True
+    for c in cols[:2]:
+        b = values[c].to_numpy()
+        got = Paillier.decrypt(ctx, res[cols.index(c)]['sum'].values, out_origin=True)
+        want = [sum(ints[b == k].tolist()) for k in res[cols.index(c)].index]
+        ok &= [int(v) for v in got] == want
+    out["dropin_groupby_bins_exact"] = bool(ok)
     return out
 
 

@@ -100,6 +100,143 @@ def histogram_groupby(fx):
     assert raw(np.array(list(agg["sum"]), dtype=object)) == want
 
 
+def _bin_sums(pub, raws, exps, bins, nbins):
+    """per-bin oracle sums (A.9) -> ([raw], [exp], [count])"""
+    from oracle import paillier_oracle as O
+    k = O.derive_public(pub.n)
+    out_r, out_e, cnt = [], [], []
+    for b in range(nbins):
+        sel = [i for i in range(len(bins)) if bins[i] == b]
+        cnt.append(len(sel))
+        r, e = O.sum_ct(k, [raws[i] for i in sel], [exps[i] for i in sel]) if sel else (1, 0)
+        out_r.append(r)
+        out_e.append(e)
+    return out_r, out_e, cnt
+
+
+def _col(df_col):
+    """raw/exponent lists of a pandas column of ciphertexts"""
+    return raw(np.array(list(df_col), dtype=object))
+
+
+def xgb_histogram_pandas(fx, resident=False):
+    """XFL's XGBoost histogram calls, verbatim, on a ciphertext column built
+    from a PaillierArray: the column keeps the flat words (PaillierDtype, no
+    object column) and each groupby sum is one segmented product, bit-exact
+    against the oracle's per-bin sums and the reference's object column.
+      - core/tree/big_feature.py:43-46 (Feature.create) and
+        xgboost/decision_tree_trainer.py:146-183 (row batches, per-feature
+        groupby agg({'count', 'sum'}), outer merge + fillna(0) + add);
+      - core/tree_ray/big_feature.py:72-75 and xgb_actor.py:340-345, 447-455
+        (groupby(observed=True)[[...]].agg, concat + groupby(index).sum)."""
+    import pandas as pd
+
+    from xfl_amd.paillier import PaillierArray
+    from xfl_amd.paillier.array import PaillierDtype
+    g = load_fixture(fx)
+    priv, pub = ctxs(g)
+    h = g["ops"]["hist"]
+    R, E = [hx(r) for r in h["ct"]["raw"]], h["ct"]["exp"]
+    n = len(R)
+    # a second, mixed-exponent column (the alignment inside the folds) and 3 features
+    a = g["ops"]["a"]
+    R2 = R[:n - 16] + [hx(r) for r in a["raw"]]
+    E2 = E[:n - 16] + list(a["exp"])
+    bins0 = list(h["bins"])
+    feats = {"f0": bins0, "f1": [(3 * b + i) % 5 for i, b in enumerate(bins0)], "f2": [(i * 7) % 3 for i in range(n)]}
+    values = pd.DataFrame({k: np.asarray(v, dtype=np.uint8) for k, v in feats.items()})
+    for RR, EE in ((R, E), (R2, E2)):
+        grad_hess = PaillierArray(np.array([_ct(pub, r, e) for r, e in zip(RR, EE)], dtype=object))
+        if resident:
+            grad_hess.to_device()
+        want = {f: _bin_sums(pub, RR, EE, b, max(b) + 1) for f, b in feats.items()}
+        # Feature.create (core/tree/big_feature.py:43-46)
+        data = pd.concat([pd.DataFrame(range(n), columns=['xfl_id']),
+                          pd.DataFrame(grad_hess, columns=['xfl_grad_hess']), values], axis=1)
+        assert isinstance(data['xfl_grad_hess'].dtype, PaillierDtype), "the ciphertext column became an object column"
+        for f in feats:
+            res = data.groupby([f])['xfl_grad_hess'].agg({'count', 'sum'})
+            wr, we, wc = want[f]
+            assert list(res['count']) == wc
+            assert _col(res['sum']) == (wr, we), f
+            assert isinstance(res['sum'].dtype, PaillierDtype)
+            # res_hist['sum'].to_numpy(): the reference's object array (decision_tree_trainer.py:180)
+            obj = res['sum'].to_numpy()
+            assert obj.dtype == object and raw(obj) == (wr, we)
+        # row batches merged as decision_tree_trainer.py:146-176 does
+        rb = 13
+        for f in feats:
+            res = None
+            for j in range((n + rb - 1) // rb):
+                b = data.iloc[rb * j: rb * (j + 1), :].groupby([f])['xfl_grad_hess'].agg({'count', 'sum'})
+                if res is None:
+                    res = b
+                    continue
+                r = pd.merge(res, b, how='outer', left_index=True, right_index=True).fillna(0)
+                r = pd.Series(b.columns).apply(lambda x: r[x + '_x'] + r[x + '_y']).T
+                r.columns = list(b.columns)
+                res = r
+            wr, we, wc = want[f]
+            assert [int(c) for c in res['count']] == wc
+            assert raw(res['sum'].to_numpy()) == (wr, we), f
+        # the reference's object column gives the same bits (pandas' object group_sum)
+        obj_data = data.copy()
+        obj_data['xfl_grad_hess'] = np.asarray(grad_hess)
+        assert obj_data['xfl_grad_hess'].dtype == object
+        ref = obj_data.groupby(['f1'])['xfl_grad_hess'].agg(['count', 'sum'])
+        got = data.groupby(['f1'])['xfl_grad_hess'].agg(['count', 'sum'])
+        assert _col(ref['sum']) == _col(got['sum'])
+        # core/tree_ray: Feature.create (big_feature.py:72-75), node concat + groupby (xgb_actor.py:340-345)
+        blocks = []
+        for lo, hi in ((0, 17), (17, n)):
+            idx = np.arange(lo, hi)
+            d = pd.DataFrame(columns=['xfl_grad_hess'] + values.columns.to_list(), index=idx)
+            d['xfl_grad_hess'] = grad_hess[lo:hi]
+            d[values.columns] = values.loc[idx, :]
+            assert isinstance(d['xfl_grad_hess'].dtype, PaillierDtype)
+            blocks.append(d)
+        agg_feature = pd.concat(blocks)
+        hist = {f: agg_feature.groupby([f], observed=True)[['xfl_grad_hess']].agg({'sum', 'count'}) for f in feats}
+        for f in feats:
+            wr, we, wc = want[f]
+            nz = [i for i in range(len(wc)) if wc[i]]
+            assert _col(hist[f][('xfl_grad_hess', 'sum')]) == ([wr[i] for i in nz], [we[i] for i in nz])
+            assert list(hist[f][('xfl_grad_hess', 'count')]) == [wc[i] for i in nz]
+        # merge_hist over per-block partial histograms (xgb_actor.py:447-455)
+        parts = [blk.groupby(['f0'], observed=True)[['xfl_grad_hess']].agg({'sum', 'count'}) for blk in blocks]
+        hist_df = pd.concat(parts)
+        merged = hist_df.groupby(hist_df.index).sum(numeric_only=False)
+        wr, we, wc = want['f0']
+        assert _col(merged[('xfl_grad_hess', 'sum')]) == (wr, we)
+        assert list(merged[('xfl_grad_hess', 'count')]) == wc
+        # Series.sum over the column = np.sum
+        from oracle import paillier_oracle as O
+        s = data['xfl_grad_hess'].sum()
+        assert (s.raw_ciphertext, s.exponent) == O.sum_ct(O.derive_public(pub.n), RR, EE)
+    # missing entries: NaN on read, skipped by the groupby sum, refused by arithmetic
+    col = pd.Series(PaillierArray(np.array([_ct(pub, r, e) for r, e in zip(R[:6], E[:6])], dtype=object)))
+    shifted = col.reindex(range(-2, 6))
+    assert shifted.isna().tolist() == [True, True] + [False] * 6
+    assert np.isnan(shifted.iloc[0])
+    grp = pd.DataFrame({"k": [0, 0, 1, 1, 1, 1, 1, 1], "c": shifted.values})
+    s = grp.groupby("k")["c"].sum()
+    k = O.derive_public(pub.n)
+    assert _col(s) == ([1, O.sum_ct(k, R[:6], E[:6])[0]], [0, O.sum_ct(k, R[:6], E[:6])[1]])
+    filled = shifted.fillna(0)
+    assert not filled.isna().any()
+    assert (filled.iloc[0].raw_ciphertext, filled.iloc[0].exponent) == (1, 0)
+    try:
+        shifted.values + shifted.values
+        raise AssertionError("arithmetic on missing ciphertexts must raise")
+    except ValueError:
+        pass
+
+
+def _ct(ctx, r, e):
+    from xfl_amd.paillier import PaillierCiphertext
+    return PaillierCiphertext(ctx, r, e)
+
+
 def decrypt_matches_reference(fx):
     """Paillier.decrypt of the reference's ciphertexts, as an object array and
     as a PaillierArray: float32 output hex-equal, out_origin values exact
@@ -164,7 +301,7 @@ def array_protocol(fx, resident=False):
         a.to_device()
         a._st.h = None  # device copy only: every host read below downloads
     R, E = raw(a_obj)
-    assert a.shape == (16,) and a.ndim == 1 and a.size == 16 and len(a) == 16 and a.dtype == object
+    assert a.shape == (16,) and a.ndim == 1 and a.size == 16 and len(a) == 16 and a.dtype.kind == "O"
     assert isinstance(a[3], PaillierCiphertext) and (a[3].raw_ciphertext, a[3].exponent) == (R[3], E[3])
     assert (a[-1].raw_ciphertext, a[-1].exponent) == (R[-1], E[-1])
     assert raw(a[2:7]) == (R[2:7], E[2:7])

@@ -31,6 +31,6 @@ int main() {
     for (int i = nw - 1; i >= 0; --i) std::printf("%08x", y[i]);
     std::printf("\n");
   }
-  std::fprintf(stderr, "fallbacks %d\n", xhe::modinv_fallbacks());
+  std::fprintf(stderr, "fallbacks %d\n", xhe::modinv_fallbacks().load());
   return 0;
 }

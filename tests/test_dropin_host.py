@@ -228,3 +228,8 @@ def test_encode_at_aligned_exponent_matches_encoder():
             assert e == min(ep, c)
             assert got == (O.encode(ok, v, ep) << (ep - e)) % priv.n, (v, ep, e)
     assert _encode_at(priv, np.array([3.0]), np.array([-2100])) is None
+
+
+@pytest.mark.parametrize("fx", HOST_FIXTURES)
+def test_xgb_histogram_pandas_columns(fx):
+    C.xgb_histogram_pandas(fx)

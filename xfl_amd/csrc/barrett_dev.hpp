@@ -254,6 +254,10 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
     for (int j = g; j < YOFF; j += G) yr[j] = 0u;
     for (int j = YOFF + S + g; j < YLEN; j += G) yr[j] = 0u;
   }
+  // Limbs change hands between the lanes of a group through LDS at every
+  // phase boundary (the operands here, then q1, q3 and r): the fence keeps
+  // each lane's stores ahead of the other lanes' loads (as k_mulmod_n2 does).
+  wave_sync_mem_();
   // ---- A: T = x y (rounds of 4G columns)
   constexpr int RA = (2 * S + RCOLS - 1) / RCOLS;
   uint32_t T[RA][4];
@@ -273,6 +277,7 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
       if (t >= S - 1 && t < 2 * S) xr[t - (S - 1)] = T[r][k];
     }
   for (int j = S + 1 + g; j < XLEN; j += G) xr[j] = 0u;
+  wave_sync_mem_();
   // ---- B: q3 = the limbs >= S+1 of q1 mu, from its columns 148 .. 307
   // (>= S-1-3: the truncation costs q3 at most 1, tools/barrett_model.py;
   // q1 mu has no column above 2S, + its carry)
@@ -294,6 +299,7 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
   // q3's x-role row ends in zeros (limbs 153, 154 were written as the zero
   // columns 306, 307; what lies beyond is y's old window)
   for (int j = S + 1 + g; j < XLEN; j += G) yr[j] = 0u;
+  wave_sync_mem_();
   // ---- C: r2 = q3 N mod beta^(4G * RC)
   constexpr int RC = (S + 1 + RCOLS - 1) / RCOLS;
   uint32_t R2[RC][4];
@@ -336,6 +342,7 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
       const int t = RCOLS * r + 4 * g + k;
       if (t < S) xr[t] = T[r][k];
     }
+  wave_sync_mem_();
   uint32_t b[M4::L];
 #pragma unroll
   for (int j = 0; j < M4::L; ++j) b[j] = xr[(g & 3) * M4::L + j];

@@ -4,6 +4,7 @@
 // (reference python/common/crypto/paillier/context.py:28-71) and the
 // Montgomery constants the device kernels need. Not on the per-element path.
 #pragma once
+#include <atomic>
 #include <stdint.h>
 
 #include <algorithm>
@@ -282,9 +283,11 @@ inline bool modinv_words_binary(const uint32_t* x32, const uint32_t* m32, int nw
 // subtract passes. Returns false when gcd(x, m) != 1; falls back to the plain
 // binary algorithm if the batch budget runs out (never observed).
 // how often modinv_words ran out of its batch budget and took the binary
-// algorithm (a test hook: the batched path is expected to always converge)
-inline int& modinv_fallbacks() {
-  static int n = 0;
+// algorithm (a test hook: the batched path is expected to always converge).
+// Atomic: inversions run on several host threads at once (one per device or
+// stream); the count is per process (never reset).
+inline std::atomic<int>& modinv_fallbacks() {
+  static std::atomic<int> n{0};
   return n;
 }
 
@@ -451,7 +454,7 @@ inline bool modinv_words(const uint32_t* x32, const uint32_t* m32, int nw32, uin
     u.swap(nu);
     v.swap(nv);
   }
-  ++modinv_fallbacks();  // never observed; tests/test_host_modinv.py asserts it stays 0
+  modinv_fallbacks().fetch_add(1, std::memory_order_relaxed);  // never observed; tests/test_host_modinv.py asserts it stays 0
   return modinv_words_binary(x32, m32, nw32, out32);
 }
 

@@ -1432,6 +1432,49 @@ int invert_impl(const xhe_key* k, const uint32_t* c, int64_t count, uint32_t* ou
   return XHE_OK;
 }
 
+// Small host -> device uploads made while enqueuing (the segment plans):
+// copied into a pinned slot whose previous copy has completed (one event per
+// slot), so the enqueue never waits for the stream. A pageable source would
+// need the stream synchronised before the frame that owns it returns - which
+// made every groupby sum wait for the previous call's kernels.
+class HostStage {
+  struct Slot {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    int dev = -1;
+  };
+  std::mutex mu_;
+  std::vector<Slot> slots_;
+
+ public:
+  void upload(void* dst, const void* src, size_t n, hipStream_t s, int dev) {
+    std::lock_guard<std::mutex> g(mu_);
+    Slot* use = nullptr;
+    for (Slot& sl : slots_)
+      if (sl.dev == dev && sl.cap >= n && hipEventQuery(sl.ev) == hipSuccess) {
+        use = &sl;
+        break;
+      }
+    if (!use) {
+      Slot sl;
+      sl.dev = dev;
+      sl.cap = std::max<size_t>(n, 64 << 10);
+      HIPCHK(hipHostMalloc(&sl.p, sl.cap, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+      slots_.push_back(sl);
+      use = &slots_.back();
+    }
+    memcpy(use->p, src, n);
+    HIPCHK(hipMemcpyAsync(dst, use->p, n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(use->ev, s));
+  }
+};
+HostStage& host_stage() {
+  static HostStage* st = new HostStage();  // process lifetime (no teardown order with the runtime)
+  return *st;
+}
+
 // Reduce segment-ordered rows [S4][count] to one Montgomery row per segment
 // (seg: nseg+1 offsets) by levels of k_chunk_prod (C rows per chunk). The
 // input rows are Montgomery rows, or plain residues with raw = true (the
@@ -1476,7 +1519,10 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
         break;
       }
     if (ones && !(first && raw)) break;  // (plain rows still need Montgomery form)
-    const int64_t C = (first && raw) || n_cur / kRawChunk >= kFill ? kRawChunk : 4;
+    // the longest chunks that still leave kFill lane groups (4 .. kRawChunk):
+    // a 100 k-row, 256-bin histogram took chunks of 32 on its first level (a
+    // 33-product chain with a quarter of the chip busy) and now takes 4
+    const int64_t C = std::max<int64_t>(4, std::min<int64_t>(kRawChunk, n_cur / kFill));
     std::vector<int64_t> nseg_b{0};
     const size_t off = all.size();
     int64_t seg_len = 0, ncs = 0;
@@ -1506,8 +1552,7 @@ uint32_t* reduce_segments(const xhe_key* k, uint32_t* rows, int64_t count, std::
   int64_t* dplan = nullptr;
   if (!all.empty()) {
     HIPCHK(hipMallocAsync((void**)&dplan, all.size() * 8, s));
-    HIPCHK(hipMemcpyAsync(dplan, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));  // `all` is host memory of this frame (one sync per call)
+    host_stage().upload(dplan, all.data(), all.size() * 8, s, k->device);  // no host sync
   }
   uint32_t* cur = rows;
   for (const Level& L : plan) {

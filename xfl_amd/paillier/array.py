@@ -24,6 +24,24 @@ Differences from an object ndarray: basic slices of a 1-D array share the
 buffers (like numpy views); other indexing returns copies; elements read
 twice are two equal PaillierCiphertext objects, not one; mutate through
 arr[i] = ciphertext, not by mutating an element read earlier.
+
+pandas: a PaillierArray is also a pandas ExtensionArray (dtype
+`PaillierDtype`, name "paillier", kind 'O'), so a DataFrame column built from
+one keeps the flat words instead of one PaillierCiphertext object per row -
+`pd.DataFrame(grad_hess, columns=['xfl_grad_hess'])` (core/tree/big_feature.py:
+43-46), `data['xfl_grad_hess'] = grad_hess` (core/tree_ray/big_feature.py:74).
+XFL's histogram calls then reach the segmented-product kernel once per call:
+`groupby(col)['xfl_grad_hess'].agg({'count', 'sum'})`
+(xgboost/decision_tree_trainer.py:151-152, core/tree_ray/xgb_actor.py:342-344)
+and `groupby(index).sum(numeric_only=False)` (xgb_actor.py:453) go through
+`_groupby_op`, `Series.sum` through `_reduce`, concat / loc / iloc / merge
+through `_concat_same_type` / `take`. Results equal pandas' object-dtype left
+folds bit for bit (the same per-group row order, `ops.fold_gap_powers`).
+Missing entries (an outer merge's reindex) are NaN on read; `fillna(0)`
+stores the unobfuscated encryption of 0 (raw 1, exponent 0), which adds
+exactly as the reference's int 0 cell does (paillier.py:93-102). Other
+groupby reductions fall back to pandas' per-group Python path over the
+PaillierCiphertext objects (the reference's semantics).
 """
 import numbers
 
@@ -33,10 +51,54 @@ from .. import _native as nat
 from . import ops, resident
 from .resident import Rows
 
+try:  # pandas is what XFL's tree operators use; without it PaillierArray is a plain class
+    from pandas.api.extensions import ExtensionArray as _EABase
+    from pandas.api.extensions import ExtensionDtype as _EADtypeBase
+    from pandas.api.extensions import register_extension_dtype as _register_dtype
+except ImportError:  # pragma: no cover - pandas is in the image
+    _EABase, _EADtypeBase = object, object
+
+    def _register_dtype(cls):
+        return cls
+
+# exponent of a missing (NA) entry: no encoder produces it (|e| < 2^31 - 1)
+NA_EXP = np.iinfo(np.int32).min
+
 
 def _ct_type():
     from .paillier import PaillierCiphertext
     return PaillierCiphertext
+
+
+@_register_dtype
+class PaillierDtype(_EADtypeBase):
+    """pandas dtype of a PaillierArray column: scalars are PaillierCiphertext,
+    missing values NaN. Not numeric (pandas' numeric_only reductions skip it,
+    as they skip the reference's object columns)."""
+    name = "paillier"
+    kind = "O"
+    na_value = np.nan
+    _is_numeric = False
+    _metadata = ()
+
+    @property
+    def type(self):
+        return _ct_type()
+
+    @classmethod
+    def construct_array_type(cls):
+        return PaillierArray
+
+    @classmethod
+    def construct_from_string(cls, string):
+        if not isinstance(string, str):
+            raise TypeError(f"'construct_from_string' expects a string, got {type(string)}")
+        if string == cls.name:
+            return cls()
+        raise TypeError(f"Cannot construct a 'PaillierDtype' from '{string}'")
+
+    def __repr__(self):
+        return "PaillierDtype()"
 
 
 def _same_key(c1, c2):
@@ -47,7 +109,7 @@ class _Fallback(Exception):
     pass
 
 
-class PaillierArray:
+class PaillierArray(_EABase):
     __array_priority__ = 1000
 
     # ------------------------------------------------------------ construction
@@ -184,7 +246,13 @@ class PaillierArray:
 
     @property
     def dtype(self):
-        return np.dtype(object)
+        """PaillierDtype (kind 'O'); np.asarray(arr).dtype is object, as for
+        the reference's arrays"""
+        return PaillierDtype() if _EADtypeBase is not object else np.dtype(object)
+
+    @property
+    def nbytes(self):
+        return self.size * (self._st.n2w * 4 + 4)
 
     @property
     def T(self):
@@ -200,9 +268,12 @@ class PaillierArray:
 
     def _elem(self, i, raw=None):
         CT = _ct_type()
+        e = int(self._e[i])
+        if e == NA_EXP:
+            return np.nan
         if raw is None:
             raw = int.from_bytes(self._w[i].tobytes(), "little")
-        return CT(self.context, raw, int(self._e[i]))
+        return CT(self.context, raw, e)
 
     def _take(self, flat_idx, shape):
         flat_idx = np.asarray(flat_idx, dtype=np.int64).reshape(-1)
@@ -234,8 +305,18 @@ class PaillierArray:
         return self._take(sel, sel.shape)
 
     def __setitem__(self, key, value):
+        key = _unbox_key(key)
         sel = np.asarray(self._index_map()[key], dtype=np.int64)
+        if _is_na(value):  # pandas' missing value (setitem / where / reindex)
+            self._e[sel.reshape(-1)] = NA_EXP
+            return
         src = _as_cipher(value)
+        if src is None and isinstance(value, numbers.Number) and not isinstance(value, complex):
+            # a plain number stored into a ciphertext column (pandas fillna(0),
+            # core/tree/...: merge(...).fillna(0)): its unobfuscated encryption,
+            # which adds exactly as the reference's number cell does
+            # (paillier.py:93-102)
+            src = _plain_cipher(self.context, value)
         if src is None:
             raise TypeError(f"can only assign PaillierCiphertext values, got {type(value)}")
         if not _same_key(src.context, self.context):
@@ -312,6 +393,8 @@ class PaillierArray:
     def astype(self, dtype, copy=True):
         """astype(object): the reference's np.ndarray[object] of
         PaillierCiphertext (as np.asarray); other dtypes convert from it."""
+        if isinstance(dtype, PaillierDtype) or dtype == PaillierDtype.name:
+            return self.copy() if copy else self
         if np.dtype(dtype) == np.dtype(object):
             return self._objects()
         return self._objects().astype(dtype)
@@ -330,6 +413,159 @@ class PaillierArray:
 
     def __reduce__(self):
         return (PaillierArray.from_buffers, (self.context, self._w, self._e, self._shape))
+
+    # ------------------------------------------------------------ pandas ExtensionArray
+    # (pandas/core/arrays/base.py's interface; 1-D arrays, as pandas uses them)
+    @classmethod
+    def _from_sequence(cls, scalars, *, dtype=None, copy=False):
+        if isinstance(scalars, PaillierArray):
+            return scalars.copy() if copy else scalars
+        arr = np.empty(len(scalars), dtype=object)
+        arr[:] = list(scalars)
+        na = np.array([_is_na(v) for v in arr], dtype=bool)
+        CT = _ct_type()
+        if not all(isinstance(v, CT) for v in arr[~na]):
+            raise TypeError("PaillierArray holds PaillierCiphertext elements")
+        if not na.any():
+            return cls(arr)
+        if na.all():
+            raise TypeError("PaillierArray._from_sequence: no ciphertext to take the key from")
+        first = arr[~na][0]
+        arr[na] = first  # placeholders, then marked missing
+        out = cls(arr)
+        out._e[na] = NA_EXP
+        return out
+
+    @classmethod
+    def _from_factorized(cls, values, original):
+        raise NotImplementedError("factorizing ciphertexts is not supported")
+
+    @classmethod
+    def _concat_same_type(cls, to_concat):
+        parts = [p.reshape(-1) for p in to_concat]
+        ctxs = [p.context for p in parts if p.context is not None]
+        if not ctxs:
+            n2w = max(p._st.n2w for p in parts)
+            parts = [p._aligned_words(n2w) for p in parts]
+            return cls.from_buffers(None, np.concatenate([p._w for p in parts]),
+                                    np.concatenate([p._e for p in parts]))
+        ctx = _ctx_of(*parts)
+        n2w = ops.n2w_of(ctx)
+        parts = [p._aligned_words(n2w) for p in parts]
+        e = np.concatenate([p._e for p in parts])
+        dev = _res_dev(ctx, *parts)
+        if dev is not None:
+            return cls.from_device(ctx, resident.cat([p._dw(dev) for p in parts]), e)
+        return cls.from_buffers(ctx, np.concatenate([p._w for p in parts]), e)
+
+    def isna(self):
+        return (self._e == NA_EXP).reshape(self._shape)
+
+    def _has_na(self):
+        return self.size > 0 and int(self._e.min()) == NA_EXP
+
+    def take(self, indices, allow_fill=False, fill_value=None):
+        """pandas take: -1 gives a missing entry when allow_fill (an outer
+        merge's reindex), numpy's negative indexing otherwise"""
+        idx = np.asarray(indices, dtype=np.int64).reshape(-1)
+        n = self.size
+        if allow_fill:
+            if idx.size and idx.min() < -1:
+                raise ValueError("take: indices below -1 with allow_fill")
+            fill = idx == -1
+        else:
+            idx = np.where(idx < 0, idx + n, idx)
+            fill = None
+        if idx.size and idx.max() >= n:
+            raise IndexError(f"take: index {int(idx.max())} out of bounds for size {n}")
+        if fill is None or not fill.any():
+            return self._take(idx, (idx.size,))
+        if n == 0:  # every entry missing
+            out = PaillierArray.from_buffers(self.context, np.zeros((idx.size, self._st.n2w), np.uint32),
+                                             np.full(idx.size, NA_EXP, np.int32))
+        else:
+            out = self._take(np.where(fill, 0, idx), (idx.size,))
+        if fill_value is None or _is_na(fill_value):
+            out._e[fill] = NA_EXP
+        else:
+            out[np.nonzero(fill)[0]] = fill_value
+        return out
+
+    def _values_for_argsort(self):
+        raise TypeError("ciphertexts have no order")
+
+    def __eq__(self, other):
+        """element-wise: equal residues and exponents (the reference's object
+        arrays compare element identity; pandas needs a value comparison)"""
+        co = _as_cipher(other)
+        if co is None:
+            return np.zeros(self._shape, dtype=bool)
+        ia, ib, shape = _bcast(self, co)
+        wa, ea = _rows(self, ia)
+        wb, eb = _rows(co._aligned_words(self._st.n2w), ib)
+        return (np.all(wa == wb, axis=1) & (ea == eb) & (ea != NA_EXP)).reshape(shape)
+
+    def __ne__(self, other):
+        return ~self.__eq__(other)
+
+    __hash__ = None
+
+    def _reduce(self, name, *, skipna=True, keepdims=False, **kwargs):
+        """Series.sum() over a ciphertext column = np.sum (order-free fold)"""
+        if name != "sum":
+            raise TypeError(f"cannot perform {name} with type {self.dtype}")
+        x = self.reshape(-1)
+        if x._has_na():
+            if not skipna:
+                return np.nan
+            x = x[~x.isna()]
+        if x.size == 0:
+            return 0  # the reference's empty object sum
+        s = _sum(x, None, False)
+        if keepdims:
+            return PaillierArray(np.array([s], dtype=object))
+        return s
+
+    def _groupby_op(self, *, how, has_dropped_na, min_count, ngroups, ids, **kwargs):
+        """groupby(...).sum() of a ciphertext column: ONE segmented product
+        (xhe_segprod) over the rows sorted stably by group, equal bit for bit
+        to pandas' object group_sum (a left fold per group in row order,
+        skipping NaN; groups with fewer than min_count values give NaN, empty
+        groups the reference's int 0 as the encryption of 0). Other
+        reductions: NotImplementedError, so pandas runs its per-group Python
+        fallback over the ciphertext objects."""
+        if how != "sum" or self.ndim != 1 or self.context is None:
+            raise NotImplementedError(f"groupby {how} over ciphertexts")
+        ctx = self.context
+        ids = np.asarray(ids).reshape(-1)
+        valid = ids >= 0
+        if self._has_na():
+            valid &= ~self.isna()
+        key = np.where(valid, ids, ngroups)
+        # stable sort by group: radix sort on narrow keys (numpy's stable sort of <= 16-bit ints)
+        key = key.astype(np.uint16 if ngroups < (1 << 16) - 1 else np.int64)
+        nvalid = int(np.count_nonzero(valid))
+        order = np.argsort(key, kind="stable")[:nvalid]
+        cnt = np.bincount(ids[valid], minlength=ngroups).astype(np.int64)
+        seg = np.zeros(ngroups + 1, dtype=np.int64)
+        np.cumsum(cnt, out=seg[1:])
+        n2w = ops.n2w_of(ctx)
+        x = self._aligned_words(n2w)
+        dev = resident.device_for(ctx, -1, x._st.count, 4 * n2w)
+        if dev is not None and (x._resident_on(dev) or x.size > SMALL):
+            x.to_device(dev)  # the whole column's words, once (every later call reads them in HBM)
+        if dev is not None and (x._resident_on(dev) or nvalid <= SMALL):
+            dw, e = _drows(x, order, dev)
+            rd, re = ops.segment_sums_dev(ctx, ctx.device_key(dev), dw, e, seg, fold=True)
+            out = PaillierArray.from_device(ctx, rd, re, (ngroups,))
+        else:
+            w, e = _rows(x, order)
+            rw, re = ops.segment_sums_words(ctx, w, e, seg, fold=True)
+            out = _result(ctx, rw, re, (ngroups,))
+        short = cnt < max(int(min_count), 1) if min_count > 0 else None
+        if short is not None and short.any():
+            out._e[short] = NA_EXP
+        return out
 
     def _aligned_words(self, n2w):
         """self with n2w-word rows (arrays decoded without a context keep the
@@ -414,6 +650,48 @@ class PaillierArray:
 
 def _unsupported(what):
     return NotImplementedError(f"PaillierArray.{what} is not supported")
+
+
+def _is_na(v):
+    """pandas' missing-value scalars (None, NaN, pd.NA)"""
+    if v is None:
+        return True
+    if isinstance(v, (float, np.floating)):
+        return bool(np.isnan(v))
+    if _EABase is not object:
+        import pandas as pd
+        return v is pd.NA or v is pd.NaT
+    return False
+
+
+def _unbox_key(key):
+    """pandas array keys (BooleanArray / IntegerArray / Index) -> numpy"""
+    if hasattr(key, "to_numpy") and not isinstance(key, (PaillierArray, np.ndarray)):
+        return key.to_numpy()
+    return key
+
+
+def _plain_cipher(ctx, value):
+    """the unobfuscated encryption of a number at its precision=None exponent,
+    1 + n m mod n^2 (paillier.py:93-102, 283), as a 0-d PaillierArray - on the
+    host (no device call for a fill value)"""
+    if ctx is None:
+        return None
+    from .encoder import PaillierEncoder
+    v = value.item() if isinstance(value, np.generic) else value
+    v = int(v) if isinstance(v, bool) else v
+    e = PaillierEncoder.cal_exponent(v, precision=None)
+    m = int(PaillierEncoder.encode_single(ctx, v, e))
+    ct = _ct_type()(ctx, (1 + ctx.n * m) % ctx.n_square, int(e))
+    return PaillierArray(np.array(ct, dtype=object).reshape(()))
+
+
+def _check_no_na(*xs):
+    """arithmetic on a missing entry raises, as the reference's ciphertext +
+    NaN does (encrypting NaN, paillier.py:93-98)"""
+    for x in xs:
+        if isinstance(x, PaillierArray) and x._has_na():
+            raise ValueError("cannot convert float NaN to integer: missing ciphertext entries (fillna first)")
 
 
 def _n2w(ctx, raws=()):
@@ -581,6 +859,7 @@ def _encrypt_plain(ctx, vals):
 def _add(a, b):
     """a + b with the reference's semantics (paillier.py:88-126)."""
     ca, cb = _as_cipher(a), _as_cipher(b)
+    _check_no_na(ca, cb)
     if ca is not None and cb is not None:
         ctx = _ctx_of(ca, cb)
         n2w = ops.n2w_of(ctx)
@@ -787,6 +1066,7 @@ def _mul(a, b):
         a, b, ca = b, a, cb
     if ca is None:
         raise _Fallback()
+    _check_no_na(ca)
     p = _as_plain(b)
     if p is None:
         if isinstance(b, (str, bytes)) or not hasattr(b, "__len__"):
@@ -830,6 +1110,7 @@ def _sum(x, axis=None, keepdims=False):
     """np.sum over ciphertexts: per output element the order-free product
     prod c_i^(2^(e_i - e_min)) (paillier.py:79-123 folded)."""
     ctx = _ctx_of(x)
+    _check_no_na(x)
     x = x._aligned_words(ops.n2w_of(ctx))
     if x.ndim == 0:
         return x._elem(0)
@@ -965,6 +1246,7 @@ def _matmul(a, b):
 
 def _matvec(A, X):
     ctx = _ctx_of(A)
+    _check_no_na(A)
     A = A._aligned_words(ops.n2w_of(ctx))
     Bn, D = X.shape
     cexp = A._e.astype(np.int64)

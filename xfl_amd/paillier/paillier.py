@@ -221,10 +221,11 @@ class Paillier(object):
         RawCiphertext, written natively from the flat words (wire.hpp)."""
         from ..compat import compress, dumps
         from . import wire
-        from .array import PaillierArray
+        from .array import PaillierArray, _check_no_na
         if isinstance(data, PaillierCiphertext):
             return data.serialize(compression)
         if isinstance(data, PaillierArray):
+            _check_no_na(data)
             out = wire.encode_words(data.words, data.exponents, data.shape)
             return compress(out) if compression else out
         if isinstance(data, np.ndarray) and data.dtype == object:
@@ -360,6 +361,8 @@ class Paillier(object):
         if not context.is_private():
             raise TypeError("Try to decrypt a paillier ciphertext by a public key.")
         if isinstance(data, PaillierArray):
+            if data._has_na():  # missing entries pass through as NaN (paillier.py:344-345: non-ciphertexts)
+                return cls.decrypt(context, data.astype(object), dtype, num_cores, out_origin)
             arr = data._aligned_words(ops.n2w_of(context))
             dev = resident.device_for(context, num_cores)
             if arr.size and (arr._resident_on(dev) or (dev is not None and arr.size <= SMALL)):

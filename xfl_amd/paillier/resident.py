@@ -148,6 +148,22 @@ def upload(a, dev):
         return torch.from_numpy(a).to(f"cuda:{dev}", non_blocking=False)
 
 
+def upload_async(a, dev):
+    """upload() without waiting: the bytes go through a pinned copy (torch's
+    caching host allocator keeps it until the copy has run) and the copy is
+    ordered on the drop-in stream of dev. For operands only the library's
+    kernels on that stream read (indices, exponents); a blocking upload
+    would wait for every kernel queued before it."""
+    torch = _torch()
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    elif a.dtype == np.uint64:
+        a = a.view(np.int64)
+    with _On(dev):
+        return torch.from_numpy(a).pin_memory().to(f"cuda:{dev}", non_blocking=True)
+
+
 def download(t, dtype=np.uint32):
     """device tensor -> host array of `dtype` (big buffers come from the
     recycled host mappings, xfl_amd._native.empty)"""
@@ -310,8 +326,8 @@ def mulmod(dk, a, ea, b, eb, dmax):
     torch = _torch()
     dev = dk.device
     n = a.shape[0]
-    eda = upload(np.ascontiguousarray(ea, dtype=np.int32), dev) if ea is not None else None
-    edb = upload(np.ascontiguousarray(eb, dtype=np.int32), dev) if eb is not None else None
+    eda = upload_async(np.ascontiguousarray(ea, dtype=np.int32), dev) if ea is not None else None
+    edb = upload_async(np.ascontiguousarray(eb, dtype=np.int32), dev) if eb is not None else None
     with _On(dev):
         out = torch.empty((n, dk.n2w), dtype=torch.int32, device=f"cuda:{dev}")
     nat.check(nat.lib().xhe_mulmod(dk.handle, _dp(a), _dp(eda), _dp(b), _dp(edb), n, int(dmax), _dp(out), None,
@@ -351,13 +367,14 @@ def segprod(dk, c, d, seg):
     d = np.ascontiguousarray(d, dtype=np.int32)
     seg = np.ascontiguousarray(seg, dtype=np.int64)
     dmax = int(d.max()) if n else 0
-    dd = upload(d, dev) if dmax else None
+    dd = upload_async(d, dev) if dmax else None
     with _On(dev):
         out = torch.empty((seg.shape[0] - 1, dk.n2w), dtype=torch.int32, device=f"cuda:{dev}")
         src = c if n else torch.zeros((1, dk.n2w), dtype=torch.int32, device=f"cuda:{dev}")
+    # the library reads `seg` while enqueuing and stages its plan through
+    # pinned memory: nothing here waits for the kernels
     nat.check(nat.lib().xhe_segprod(dk.handle, _dp(src), _dp(dd), dmax, n, seg.ctypes.data_as(ctypes.c_void_p),
                                     seg.shape[0] - 1, _dp(out), _sp(dev)), "segprod")
-    stream(dev).synchronize()  # seg is a host array the library reads while enqueuing; keep it alive till done
     return out
 
 
@@ -392,7 +409,9 @@ def take(c, idx):
     with _On(dev):
         out = torch.empty((idx.shape[0],) + tuple(c.shape[1:]), dtype=c.dtype, device=c.device)
     if idx.shape[0]:
-        ii = upload(idx, dev)
+        if idx.min() < 0 or idx.max() >= c.shape[0]:
+            raise IndexError(f"take: row index out of range for {c.shape[0]} rows")
+        ii = upload_async(idx, dev)
         nat.check(nat.lib().xhe_gather_rows(_dp(c), _dp(ii), idx.shape[0], _row_words(c), _dp(out), _sp(dev)),
                   "gather_rows")
     return out
@@ -428,7 +447,13 @@ def put_rows(c, idx, rows):
     dev = c.device.index
     idx = np.ascontiguousarray(idx, dtype=np.int64)
     if idx.shape[0]:
-        ii = upload(idx, dev)
-        src = rows.contiguous()
+        if idx.min() < 0 or idx.max() >= c.shape[0] or np.unique(idx).shape[0] != idx.shape[0]:
+            raise IndexError(f"put_rows: indices must be distinct rows of the {c.shape[0]}")
+        if tuple(rows.shape) != (idx.shape[0],) + tuple(c.shape[1:]) or rows.dtype != c.dtype:
+            raise ValueError(f"put_rows: rows {tuple(rows.shape)} {rows.dtype} for {idx.shape[0]} rows of {tuple(c.shape)} "
+                             f"{c.dtype}")
+        ii = upload_async(idx, dev)
+        with _On(dev):  # a copy made on the drop-in stream, ordered before the scatter that reads it
+            src = rows.contiguous()
         nat.check(nat.lib().xhe_scatter_rows(_dp(src), _dp(ii), idx.shape[0], _row_words(c), _dp(c), _sp(dev)),
                   "scatter_rows")
