@@ -132,6 +132,10 @@ int xhe_gather_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t cou
                     void* stream);
 int xhe_scatter_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t count, int words, uint32_t* dst_dev,
                      void* stream);
+/* bits_dev[i] = bit length of row i of words_dev (count x n2w little-endian
+ * words, n2w <= 1023): the per-element input of xhe_wire_layout, so the
+ * serialize payload is sized before the ciphertexts are downloaded. */
+int xhe_row_bits(const uint32_t* words_dev, int64_t count, int n2w, int16_t* bits_dev, void* stream);
 
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
 int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* k,
@@ -172,6 +176,25 @@ int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int 
                     uint8_t* out, int64_t cap, int64_t* out_len);
 int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
                     int64_t* count, int64_t* shape, int* ndim);
+/* xhe_wire_encode written straight into its final bytes: framed == 0 gives
+ * the same pickle; framed != 0 gives xhe_zstd_raw_frame(pickle) - what
+ * Paillier.serialize(compression=True) sends (paillier.py:244-258) - without
+ * the intermediate pickle buffer. *out_len = the bytes needed; XHE_EOVERFLOW
+ * when cap is smaller (out may be NULL). */
+int xhe_wire_encode_frame(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,
+                          int ndim, int framed, uint8_t* out, int64_t cap, int64_t* out_len);
+/* The same bytes in two steps, for words that arrive chunk by chunk (the
+ * serialize pipeline overlaps the D2H copy of one chunk with the encoding of
+ * the previous one). layout: elem_off[0..count] = each element's pickle
+ * offset (elem_off[count]: the footer), from the bit lengths (xhe_row_bits);
+ * *out_len = the payload size; with out (cap >= it) also the header, the
+ * footer and, framed, the zstd frame and block headers. rows: elements
+ * lo..hi-1 (rows[0] = element lo) at those offsets; XHE_EINVAL when a row's
+ * bit length differs from the layout's. */
+int xhe_wire_layout(const int16_t* bits, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                    int framed, int64_t* elem_off, uint8_t* out, int64_t cap, int64_t* out_len);
+int xhe_wire_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                  const int64_t* elem_off, int framed, uint8_t* out, int64_t cap);
 
 /* A zstd frame (RFC 8878, one frame, content size in the header) holding
  * src[0..n) as raw blocks, written by several host threads: what

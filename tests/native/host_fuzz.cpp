@@ -167,6 +167,51 @@ static void own_format(std::mt19937_64& rng) {
       Bytes ref((size_t)xhe::wire::encode_reference(ct.data(), ex.data(), count, n2w, shape, 2, nullptr, 0));
       xhe::wire::encode_reference(ct.data(), ex.data(), count, n2w, shape, 2, ref.data(), (int64_t)ref.size());
       if (ref != out) std::abort();  // the fast writer produces the specification's bytes
+      // the one-pass writer (encode_to) through a plain sink, and through a
+      // framed sink with small blocks (payloads split across block borders)
+      {
+        Bytes flat((size_t)need);
+        const xhe::wire::Sink plain{flat.data(), 0};
+        if (xhe::wire::encode_to(ct.data(), ex.data(), count, n2w, shape, 2, &plain, threads) != need) std::abort();
+        if (flat != out) std::abort();
+        // layout from bit lengths + rows in chunks (the serialize pipeline)
+        std::vector<int16_t> bits((size_t)std::max<int64_t>(count, 1), 0);
+        for (int64_t i = 0; i < count; ++i) {
+          int k = n2w - 1;
+          while (k >= 0 && ct[(size_t)i * n2w + k] == 0) --k;
+          bits[i] = (int16_t)(k < 0 ? 0 : 32 * k + 32 - __builtin_clz(ct[(size_t)i * n2w + k]));
+        }
+        std::vector<int64_t> offs((size_t)count + 1);
+        Bytes piece((size_t)need, 0xEE);
+        const xhe::wire::Sink ps{piece.data(), 0};
+        if (xhe::wire::layout(bits.data(), ex.data(), count, n2w, shape, 2, offs.data(), &ps, threads) != need)
+          std::abort();
+        for (int64_t lo = 0; lo < count; lo += 777) {
+          const int64_t hi = std::min<int64_t>(count, lo + 777);
+          if (!xhe::wire::write_rows(ct.data() + (size_t)lo * n2w, ex.data(), lo, hi, count, n2w, offs.data(), ps,
+                                     threads))
+            std::abort();
+        }
+        if (piece != out) std::abort();
+        if (count > 1) {  // a wrong bit length is refused
+          bits[1] = (int16_t)(bits[1] > 8 ? bits[1] - 8 : bits[1] + 8);
+          xhe::wire::layout(bits.data(), ex.data(), count, n2w, shape, 2, offs.data(), nullptr, threads);
+          if (xhe::wire::write_rows(ct.data(), ex.data(), 0, count, count, n2w, offs.data(), ps, threads)) std::abort();
+        }
+        for (int64_t blk : {(int64_t)1, (int64_t)37, (int64_t)1000, (int64_t)131072}) {
+          const int64_t nbk = (need + blk - 1) / blk;
+          Bytes fr((size_t)(14 + need + 3 * nbk), 0xEE);
+          const xhe::wire::Sink framed{fr.data(), blk};
+          xhe::wire::encode_to(ct.data(), ex.data(), count, n2w, shape, 2, &framed, threads);
+          for (int64_t b = 0; b < nbk; ++b) {
+            const int64_t len = std::min<int64_t>(blk, need - b * blk);
+            const uint8_t* pay = fr.data() + 14 + b * (blk + 3) + 3;
+            if (std::memcmp(pay, out.data() + b * blk, (size_t)len)) std::abort();
+            for (int k = 0; k < 3; ++k)  // block headers untouched (the caller writes them)
+              if (fr[(size_t)(14 + b * (blk + 3) + k)] != 0xEE) std::abort();
+          }
+        }
+      }
       const int64_t cap = std::max<int64_t>(count, 1);
       std::vector<uint32_t> a((size_t)cap * n2w), b((size_t)cap * n2w);
       std::vector<int32_t> ea(cap), eb(cap);

@@ -64,6 +64,13 @@ SIGNATURES = {
     "xhe_decrypt_decode_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp]),
     "xhe_wire_encode": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, _vp,
                                        ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "xhe_wire_encode_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int,
+                                             _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "xhe_wire_layout": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, _vp,
+                                       _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "xhe_wire_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
+                                     ctypes.c_int, _vp, ctypes.c_int64]),
+    "xhe_row_bits": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
     "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64), _vp, ctypes.POINTER(ctypes.c_int)]),
     "xhe_host_prefault": (ctypes.c_int, [_vp, ctypes.c_int64]),
@@ -165,6 +172,61 @@ def advise_huge(addr, nbytes):
             _libc.madvise(lo, hi - lo, _MADV_HUGEPAGE)
     except (OSError, AttributeError):
         pass
+
+
+_M_TRIM_THRESHOLD, _M_MMAP_MAX, _M_MMAP_MAX_DEFAULT = -1, -4, 65536
+_heap_lock = threading.Lock()
+_heap_ready = False
+HEAP_PAYLOAD_MAX = (1 << 31) - 1  # payloads up to this size come from the heap (below); mallopt takes an int
+
+
+def _pybytes(n):
+    f = ctypes.pythonapi.PyBytes_FromStringAndSize
+    f.restype = ctypes.py_object
+    f.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+    return f(None, n)
+
+
+def alloc_bytes(n):
+    """An UNINITIALISED bytes object of n bytes for the library to fill
+    completely (the serialize payloads: Paillier.serialize returns bytes,
+    paillier.py:244-258). Payloads of 32 MiB up to HEAP_PAYLOAD_MAX are taken
+    from glibc's main heap rather than a fresh mapping: on the GPU box a
+    545 MB mapping cost its first-touch faults and ~30 ms more when it was
+    unmapped (the kernel zeroes freed pages), once per payload; a heap block
+    freed by the caller stays in the heap's free list (trimming raised to
+    2 GiB) and the next payload of a training loop lands in the same, already
+    mapped pages. Main thread only (another thread's arena cannot grow that
+    far without mmap); $XHE_HEAP_PAYLOADS=0 turns it off."""
+    global _heap_ready
+    n = int(n)
+    if n < 2:
+        raise ValueError("alloc_bytes: bytes objects below 2 bytes are shared singletons")
+    if n < (32 << 20) or n > HEAP_PAYLOAD_MAX or os.environ.get("XHE_HEAP_PAYLOADS", "1").strip() == "0" or \
+            threading.current_thread() is not threading.main_thread():
+        b = _pybytes(n)
+        advise_huge(ctypes.cast(b, ctypes.c_void_p).value, n)
+        return b
+    global _libc
+    with _heap_lock:
+        try:
+            if _libc is None:
+                _libc = ctypes.CDLL(None)
+                _libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            _libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
+            if not _heap_ready:
+                _libc.mallopt(_M_TRIM_THRESHOLD, HEAP_PAYLOAD_MAX)  # freed payload blocks stay in the heap
+                _heap_ready = True
+            _libc.mallopt(_M_MMAP_MAX, 0)
+            try:
+                return _pybytes(n)
+            finally:
+                _libc.mallopt(_M_MMAP_MAX, _M_MMAP_MAX_DEFAULT)
+        except (MemoryError, OSError, AttributeError):
+            pass
+    b = _pybytes(n)
+    advise_huge(ctypes.cast(b, ctypes.c_void_p).value, n)
+    return b
 
 
 class _HostBlock:

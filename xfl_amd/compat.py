@@ -139,9 +139,8 @@ def compress(data: bytes, level: int = 3) -> bytes:
         from . import _native as nat
         L = nat.lib()
         size = L.xhe_zstd_raw_frame_size(len(data))
-        out = bytes(size)  # written in place; nothing else references it yet
+        out = nat.alloc_bytes(size)  # written in place (every byte); nothing else references it yet
         ptr = ctypes.cast(out, ctypes.c_void_p)
-        nat.advise_huge(ptr.value, size)
         n = ctypes.c_int64()
         nat.check(L.xhe_zstd_raw_frame(data, len(data), ptr, size, ctypes.byref(n)), "zstd frame")
         return out
@@ -164,9 +163,8 @@ def _raw_extract(data):
     n = ctypes.c_int64()
     if L.xhe_zstd_raw_extract(data, len(data), None, 0, ctypes.byref(n)) != nat.XHE_EOVERFLOW or n.value < 2:
         return None
-    out = bytes(n.value)
+    out = nat.alloc_bytes(n.value)  # every byte written by the extract
     ptr = ctypes.cast(out, ctypes.c_void_p)
-    nat.advise_huge(ptr.value, n.value)
     nat.check(L.xhe_zstd_raw_extract(data, len(data), ptr, n.value, ctypes.byref(n)), "zstd extract")
     return out
 
@@ -186,7 +184,8 @@ def decompress(data: bytes) -> bytes:
         if L.ZSTD_isError(n):
             raise RuntimeError("zstd decompression failed")
         return ctypes.string_at(dst, n)
-    out = bytes(int(size))  # written in place: the frame fills it exactly
+    from . import _native as nat
+    out = nat.alloc_bytes(int(size))  # written in place: the frame fills it exactly
     n = L.ZSTD_decompress(ctypes.cast(out, ctypes.c_void_p), int(size), data, len(data))
     if L.ZSTD_isError(n) or n != size:
         raise RuntimeError("zstd decompression failed")

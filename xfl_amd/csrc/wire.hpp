@@ -300,6 +300,181 @@ inline int64_t encode(const uint32_t* ct, const int32_t* exps, int64_t count, in
   return total;
 }
 
+// Where the bytes of `encode` go: straight (pos -> out + pos) or as the
+// content of one zstd frame of raw blocks of `blk` bytes (14-byte frame
+// header, 3-byte block headers; pos -> its block's payload).
+struct Sink {
+  uint8_t* out;
+  int64_t blk;  // 0: unframed
+  void copy(int64_t pos, const uint8_t* src, int64_t len) const {
+    if (!blk) {
+      memcpy(out + pos, src, (size_t)len);
+      return;
+    }
+    while (len > 0) {
+      const int64_t b = pos / blk, in = pos - b * blk, n = std::min(len, blk - in);
+      memcpy(out + 14 + b * (blk + 3) + 3 + in, src, (size_t)n);
+      pos += n;
+      src += n;
+      len -= n;
+    }
+  }
+};
+
+// `encode` written through a Sink: every thread encodes its element range
+// into a small local buffer (cache-resident) and copies it to the Sink's
+// positions, so a framed payload is written once, not as a pickle and then
+// again as the frame (the intermediate pickle cost its own page faults and a
+// ~30 ms munmap per 1 M ciphertexts on the GPU box). Returns the pickle's
+// byte count; writes nothing when out == nullptr (size query).
+inline int64_t encode_to(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,
+                         int ndim, const Sink* sink, int threads = 1) {
+  Writer hw{nullptr, 0};
+  emit_header(hw, shape, ndim);
+  const int64_t head = hw.n;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, count / 4096));
+  std::vector<int64_t> part(T + 1, 0);
+  for (int t = 0; t <= T; ++t) part[t] = count * t / T;
+  std::vector<int64_t> bytes(T, 0);
+  run_parallel(T, [&](int t) {
+    int64_t b = 0;
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) b += elem_bytes(ct + (size_t)i * n2w, n2w, exps[i], i, count);
+    bytes[t] = b;
+  });
+  std::vector<int64_t> off(T + 1, head);
+  for (int t = 0; t < T; ++t) off[t + 1] = off[t] + bytes[t];
+  const int64_t total = off[T] + 3;
+  if (!sink) return total;
+  {
+    std::vector<uint8_t> hb((size_t)head);
+    Writer h{hb.data(), head};
+    emit_header(h, shape, ndim);
+    sink->copy(0, hb.data(), head);
+  }
+  run_parallel(T, [&](int t) {
+    constexpr int64_t kBuf = 64 << 10;
+    std::vector<uint8_t> loc((size_t)kBuf + 8192);  // + one element's bytes of headroom
+    int64_t pos = off[t], fill = 0;
+    int64_t i = part[t];
+    if (i == 0 && i < part[t + 1]) {
+      Writer w{loc.data(), (int64_t)loc.size()};
+      emit_elem(w, ct, n2w, exps[0], 0, count);
+      fill = w.n;
+      ++i;
+    }
+    for (; i < part[t + 1]; ++i) {
+      fill = write_elem(loc.data() + fill, ct + (size_t)i * n2w, n2w, exps[i], i, count) - loc.data();
+      if (fill >= kBuf) {
+        sink->copy(pos, loc.data(), fill);
+        pos += fill;
+        fill = 0;
+      }
+    }
+    if (fill) sink->copy(pos, loc.data(), fill);
+  });
+  uint8_t foot[3];
+  Writer f{foot, 3};
+  emit_footer(f);
+  sink->copy(off[T], foot, 3);
+  return total;
+}
+
+// ---- the same bytes in two steps, for rows that arrive in pieces (the
+// serialize pipeline: bit lengths first, then the words chunk by chunk).
+// An element's size depends on its value only through the bit length.
+inline int64_t elem_bytes_bits(int bits, int n2w, int32_t e, int64_t i, int64_t count) {
+  if (i == 0) {  // a row of that bit length: the same LONG size as the value
+    std::vector<uint32_t> row((size_t)n2w, 0u);
+    if (bits > 0) row[(size_t)(bits - 1) / 32] = 1u << ((bits - 1) % 32);
+    return elem_bytes(row.data(), n2w, e, 0, count);
+  }
+  const int64_t nb = bits == 0 ? 0 : (bits + 8) / 8;
+  int64_t s = 8 + (nb < 256 ? 2 : 5) + nb + 2 + ((e >= 0 && e < 256) ? 2 : 5) + 2;
+  if (i % 1000 == 0) s += 1;
+  if (i % 1000 == 999 || i == count - 1) s += 1;
+  return s;
+}
+
+// Pickle offsets off[0..count] of every element (off[count]: the footer)
+// from the bit lengths; returns the pickle's byte count. With a sink, also
+// writes the header and the footer (rows go through write_rows).
+inline int64_t layout(const int16_t* bits, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,
+                      int ndim, int64_t* off, const Sink* sink, int threads = 1) {
+  Writer hw{nullptr, 0};
+  emit_header(hw, shape, ndim);
+  const int64_t head = hw.n;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, count / 4096));
+  std::vector<int64_t> part(T + 1, 0), tot(T + 1, 0);
+  for (int t = 0; t <= T; ++t) part[t] = count * t / T;
+  run_parallel(T, [&](int t) {  // per-part sizes into off[] (exclusive prefix inside the part)
+    int64_t b = 0;
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) {
+      off[i] = b;
+      b += elem_bytes_bits(bits[i], n2w, exps[i], i, count);
+    }
+    tot[t + 1] = b;
+  });
+  tot[0] = head;
+  for (int t = 0; t < T; ++t) tot[t + 1] += tot[t];
+  run_parallel(T, [&](int t) {
+    for (int64_t i = part[t]; i < part[t + 1]; ++i) off[i] += tot[t];
+  });
+  off[count] = tot[T];
+  const int64_t total = tot[T] + 3;
+  if (sink) {
+    std::vector<uint8_t> hb((size_t)head);
+    Writer h{hb.data(), head};
+    emit_header(h, shape, ndim);
+    sink->copy(0, hb.data(), head);
+    uint8_t foot[3];
+    Writer f{foot, 3};
+    emit_footer(f);
+    sink->copy(tot[T], foot, 3);
+  }
+  return total;
+}
+
+// Elements lo .. hi-1 (rows: their words, row lo first) at the offsets of
+// `layout`. Returns false when a row's size disagrees with its offsets (its
+// bit length was not the one the layout was made from).
+inline bool write_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                       const int64_t* off, const Sink& sink, int threads = 1) {
+  const int64_t n = hi - lo;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / 2048));
+  std::vector<char> ok((size_t)T, 1);
+  run_parallel(T, [&](int t) {
+    constexpr int64_t kBuf = 64 << 10;
+    std::vector<uint8_t> loc((size_t)kBuf + 8192);
+    const int64_t a = lo + n * t / T, b = lo + n * (t + 1) / T;
+    int64_t pos = off[a], fill = 0;
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t* row = rows + (size_t)(i - lo) * n2w;
+      int64_t len;
+      if (i == 0) {
+        Writer w{loc.data() + fill, (int64_t)loc.size() - fill};
+        emit_elem(w, row, n2w, exps[0], 0, count);
+        len = w.n;
+      } else {
+        len = write_elem(loc.data() + fill, row, n2w, exps[i], i, count) - (loc.data() + fill);
+      }
+      if (len != off[i + 1] - off[i]) {
+        ok[t] = 0;
+        return;
+      }
+      fill += len;
+      if (fill >= kBuf) {
+        sink.copy(pos, loc.data(), fill);
+        pos += fill;
+        fill = 0;
+      }
+    }
+    if (fill) sink.copy(pos, loc.data(), fill);
+  });
+  for (char c : ok)
+    if (!c) return false;
+  return true;
+}
+
 // The same bytes written one put() at a time (the specification the fast
 // encoder is checked against in tests/native/host_fuzz.cpp).
 inline int64_t encode_reference(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,

@@ -168,6 +168,84 @@ int xhe_wire_encode(const uint32_t* ct, const int32_t* exps, int64_t count, int 
   });
 }
 
+namespace {
+// frame header + every block header of a raw-block frame holding pk content bytes
+void write_frame_headers(uint8_t* out, int64_t pk) {
+  static const uint8_t head[6] = {0x28, 0xB5, 0x2F, 0xFD, 0xC0, (uint8_t)((kZstdWindowLog - 10) << 3)};
+  memcpy(out, head, 6);
+  for (int k = 0; k < 8; ++k) out[6 + k] = (uint8_t)((uint64_t)pk >> (8 * k));
+  const int64_t nb = (pk + kZstdBlock - 1) / kZstdBlock;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t len = std::min<int64_t>(kZstdBlock, pk - b * kZstdBlock);
+    const uint32_t h = (uint32_t)(b == nb - 1) | ((uint32_t)len << 3);  // Last_Block, Raw, Block_Size
+    uint8_t* o = out + 14 + b * (kZstdBlock + 3);
+    o[0] = (uint8_t)h;
+    o[1] = (uint8_t)(h >> 8);
+    o[2] = (uint8_t)(h >> 16);
+  }
+}
+}  // namespace
+
+int xhe_wire_encode_frame(const uint32_t* ct, const int32_t* exps, int64_t count, int n2w, const int64_t* shape,
+                          int ndim, int framed, uint8_t* out, int64_t cap, int64_t* out_len) {
+  return guarded([&]() -> int {
+    if (!out_len || count < 0 || n2w <= 0 || ndim < 0 || ndim > 8 || (count > 0 && (!ct || !exps)) ||
+        (ndim > 0 && !shape))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_encode_frame: bad argument");
+    int64_t prod = 1;
+    for (int d = 0; d < ndim; ++d) prod *= shape[d];
+    if (prod != count) return xhe_fail(XHE_EINVAL, "xhe_wire_encode_frame: shape does not match count");
+    const int T = codec_threads();
+    const int64_t pk = xhe::wire::encode_to(ct, exps, count, n2w, shape, ndim, nullptr, T);
+    const int64_t need = framed ? xhe_zstd_raw_frame_size(pk) : pk;
+    *out_len = need;
+    if (!out || need > cap) return xhe_fail(XHE_EOVERFLOW, "xhe_wire_encode_frame: output buffer too small");
+    if (framed) write_frame_headers(out, pk);  // those of xhe_zstd_raw_frame(pickle); the pickle into the payloads
+    const xhe::wire::Sink sink{out, framed ? kZstdBlock : 0};
+    xhe::wire::encode_to(ct, exps, count, n2w, shape, ndim, &sink, T);
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_layout(const int16_t* bits, const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim,
+                    int framed, int64_t* elem_off, uint8_t* out, int64_t cap, int64_t* out_len) {
+  return guarded([&]() -> int {
+    if (!out_len || !elem_off || count < 0 || n2w <= 0 || n2w > 1023 || ndim < 0 || ndim > 8 ||
+        (count > 0 && (!bits || !exps)) || (ndim > 0 && !shape))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_layout: bad argument");
+    int64_t prod = 1;
+    for (int d = 0; d < ndim; ++d) prod *= shape[d];
+    if (prod != count) return xhe_fail(XHE_EINVAL, "xhe_wire_layout: shape does not match count");
+    for (int64_t i = 0; i < count; ++i)
+      if (bits[i] < 0 || bits[i] > 32 * n2w) return xhe_fail(XHE_EINVAL, "xhe_wire_layout: bit length out of range");
+    const int T = codec_threads();
+    const int64_t pk = xhe::wire::layout(bits, exps, count, n2w, shape, ndim, elem_off, nullptr, T);
+    const int64_t need = framed ? xhe_zstd_raw_frame_size(pk) : pk;
+    *out_len = need;
+    if (!out) return XHE_OK;
+    if (need > cap) return xhe_fail(XHE_EOVERFLOW, "xhe_wire_layout: output buffer too small");
+    if (framed) write_frame_headers(out, pk);
+    const xhe::wire::Sink sink{out, framed ? kZstdBlock : 0};
+    xhe::wire::layout(bits, exps, count, n2w, shape, ndim, elem_off, &sink, T);
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                  const int64_t* elem_off, int framed, uint8_t* out, int64_t cap) {
+  return guarded([&]() -> int {
+    if (!rows || !exps || !elem_off || !out || lo < 0 || hi < lo || hi > count || n2w <= 0 || n2w > 1023)
+      return xhe_fail(XHE_EINVAL, "xhe_wire_rows: bad argument");
+    const int64_t pk = elem_off[count] + 3;
+    if ((framed ? xhe_zstd_raw_frame_size(pk) : pk) > cap)
+      return xhe_fail(XHE_EOVERFLOW, "xhe_wire_rows: output buffer smaller than the layout");
+    const xhe::wire::Sink sink{out, framed ? kZstdBlock : 0};
+    if (!xhe::wire::write_rows(rows, exps, lo, hi, count, n2w, elem_off, sink, codec_threads()))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_rows: a row's bit length differs from the layout's");
+    return XHE_OK;
+  });
+}
+
 int xhe_wire_decode(const uint8_t* data, int64_t len, int n2w, uint32_t* ct, int32_t* exps, int64_t cap_count,
                     int64_t* count, int64_t* shape, int* ndim) {
   return guarded([&]() -> int {

@@ -2245,7 +2245,32 @@ __global__ void k_move_rows(const uint32_t* __restrict__ src, const int64_t* __r
   }
 }
 
+// bit length of each row's value (little-endian words, row-major): what the
+// wire layout of Paillier.serialize needs per element (its LONG1/LONG4 byte
+// count, paillier.py:244-258), so the host can size the payload before the
+// ciphertext words come down
+__global__ void k_row_bits(const uint32_t* __restrict__ w, int64_t count, int n2w, int16_t* __restrict__ bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t* r = w + (size_t)i * n2w;
+  int k = n2w - 1;
+  while (k >= 0 && r[k] == 0u) --k;
+  bits[i] = (int16_t)(k < 0 ? 0 : 32 * k + 32 - __clz((int)r[k]));
+}
+
 extern "C" {
+
+int xhe_row_bits(const uint32_t* words_dev, int64_t count, int n2w, int16_t* bits_dev, void* stream) {
+  return guarded([&]() -> int {
+    if (count < 0 || n2w <= 0 || n2w > 1023) return fail(XHE_EINVAL, "xhe_row_bits: bad size");
+    if (count == 0) return XHE_OK;
+    if (!words_dev || !bits_dev) return fail(XHE_EINVAL, "xhe_row_bits: null argument");
+    hipLaunchKernelGGL(k_row_bits, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       words_dev, count, n2w, bits_dev);
+    HIPCHK(hipGetLastError());
+    return XHE_OK;
+  });
+}
 
 int xhe_key_create(int device, int key_bits, const uint32_t* n_words, const uint32_t* p_words,
                    const uint32_t* q_words, const uint32_t* h_pow_n_words, int win_bits, xhe_key** out) {

@@ -226,8 +226,14 @@ class Paillier(object):
             return data.serialize(compression)
         if isinstance(data, PaillierArray):
             _check_no_na(data)
-            out = wire.encode_words(data.words, data.exponents, data.shape)
-            return compress(out) if compression else out
+            st = data._st
+            if st.h is None and st.d is not None and data.size >= wire.PIPE_MIN:
+                # words only in HBM (a fresh encryption or operation result):
+                # laid out from their bit lengths, downloaded and encoded in
+                # overlapping chunks
+                dev = st.d.device.index
+                return wire.encode_device(data._dw(dev), data.exponents, data.shape, compression, dev)
+            return wire.encode_words(data.words, data.exponents, data.shape, compression=compression)
         if isinstance(data, np.ndarray) and data.dtype == object:
             flat = list(data.reshape(-1))
             materialize(flat)
@@ -235,8 +241,9 @@ class Paillier(object):
                 raws = [x.raw_ciphertext for x in flat]
                 ctx = flat[0].context
                 bits = ctx.n_square.bit_length() if ctx is not None else max(r.bit_length() for r in raws)
-                out = wire.encode(raws, [x.exponent for x in flat], data.shape, max(1, (bits + 31) // 32))
-                return compress(out) if compression else out
+                n2w = max(1, (bits + 31) // 32)
+                ct = nat.ints_to_words(raws, n2w) if raws else np.zeros((0, n2w), np.uint32)
+                return wire.encode_words(ct, [x.exponent for x in flat], data.shape, compression=compression)
 
         def f(x):
             return RawCiphertext(x.raw_ciphertext, x.exponent)

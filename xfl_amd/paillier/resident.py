@@ -241,16 +241,27 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
     prec = -1 if precision is None else int(precision)
     has_max = max_exponent is not None
     s = _sp(dev)
+    es_h = None
     for lo in range(0, n, c):
         k = min(c, n - lo)
         nat.check(L.xhe_encode_f64(dk.handle, _dp(xd[lo:]), k, prec, int(has_max),
                                    int(max_exponent) if has_max else 0, _dp(m), _dp(es[0, lo:]), _dp(es[1, lo:]), s),
                   "encrypt")
+        if n <= c:
+            # one pass: the exponents and statuses come back as soon as the
+            # encoder has run (a bad input raises before any encryption is
+            # queued, as the reference raises in encode), and the encryption
+            # kernels are left running - the caller's next step (serialize's
+            # D2H, another operation) is ordered after them on this stream
+            es_h = download(es, np.int32)
+            if np.any(es_h[1] != 0):
+                return ct, es_h[0].copy(), es_h[1].copy()
         if obfuscation:
             seed, nonce = _seed()
             nat.check(L.xhe_rand(dk.handle, seed, nonce, k, _dp(rnd), None, s), "rand")
         nat.check(L.xhe_encrypt(dk.handle, _dp(m), _dp(rnd), k, _dp(ct[lo:]), s), "encrypt")
-    es_h = download(es, np.int32)
+    if es_h is None:
+        es_h = download(es, np.int32)
     return ct, es_h[0].copy(), es_h[1].copy()
 
 
