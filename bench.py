@@ -138,6 +138,122 @@ def pmc_traffic(win_bits, n, kernel="k_djn_pmd"):
     return None, None, None
 
 
+def sliding_window_ops(e, w=5):
+    """(squarings, products) of the kernels' wave-uniform sliding-window
+    schedule for the exponent e (pow_uniform_exp / pmd_pow_uniform): the
+    table x, x^3 .. x^31 (one squaring, 15 products), the first window's odd
+    power as the start value, then per zero bit a squaring and per window
+    [i..j] its i - j + 1 squarings and one product"""
+    bits = bin(e)[2:]
+    sq, mul = 1, 2 ** (w - 1) - 1
+    i = 0
+    i += min(w, len(bits))
+    while i and bits[i - 1] == "0":  # the window ends in a set bit
+        i -= 1
+    while i < len(bits):
+        if bits[i] == "0":
+            sq += 1
+            i += 1
+            continue
+        j = min(len(bits), i + w)
+        while bits[j - 1] == "0":
+            j -= 1
+        sq += j - i
+        mul += 1
+        i = j
+    return sq, mul
+
+
+def barrett_add_mads():
+    """v_mad_u64_u32 lane-instructions per element of k_add_barrett
+    (barrett_dev.hpp): every round walks the union of its 32 columns' terms
+    in pairs of 4-term blocks, 8 lanes x 4 columns"""
+    S, RC = 152, 32
+
+    def cols(C0, LX, LY):
+        ilo = max(0, C0 - (LY - 1))
+        ihi = min(LX - 1, C0 + RC - 1)
+        ib0 = ilo & ~3
+        return ((ihi + 1 - ib0 + 7) >> 3) * 8 * 4 * 8  # npair pairs x 8 terms x 4 columns x 8 lanes
+    a = sum(cols(RC * r, S, S) for r in range((2 * S + RC - 1) // RC))
+    b0 = S - 4
+    b = sum(cols(b0 + RC * r, S + 1, S + 1) for r in range((2 * S + 2 - b0 + RC - 1) // RC))
+    c = sum(cols(RC * r, S + 1, S) for r in range((S + 1 + RC - 1) // RC))
+    return a + b + c
+
+
+def issued_mads(bits, key_material, win_bits):
+    """v_mad_u64_u32 lane-instructions per operation from each kernel's
+    schedule (DESIGN 4: digit product 5 K^2, digit squaring 4 K^2 at K = 37
+    mod P^2 (28-bit limbs) and K = 80 mod n^2 (27-bit); Montgomery product
+    2 S^2 at S = 74 mod P^2 and S = 152 mod n^2), for the 2048-bit kernels
+    the ops figures time; the dominant kernel of each operation, conversions
+    and CRT left out (a lower bound on what was issued)"""
+    if bits != 2048:
+        return {}
+    p, q, n, _ = key_material
+    from xfl_amd import _native as nat
+    dsq, dmul, nsq, nmul, mp2, mn2 = 4 * 37 ** 2, 5 * 37 ** 2, 4 * 80 ** 2, 5 * 80 ** 2, 2 * 74 ** 2, 2 * 152 ** 2
+    rand_bits = n.bit_length() // 2
+    out = {}
+    nwin = nat.win_layout(rand_bits, win_bits)[0]
+    out["headline"] = 2 * ((nwin - 1) * dmul + 37 ** 2 + 2 * mp2)  # k_djn_pmd: table products, to_mont2, (1 + n m)
+    sp, mp = sliding_window_ops(p - 1)
+    sq_, mq = sliding_window_ops(q - 1)
+    out["decrypt_per_s"] = (sp + sq_) * dsq + (mp + mq) * dmul  # k_dec_pmd_pow, x^(P-1) per prime
+    out["add_per_s"] = barrett_add_mads()
+    out["sum_per_s"] = int(1.035 * mn2)  # k_chunk_prod_words: ~1 product per element (+1 per chunk, upper levels)
+    out["encrypt_public_djn_per_s"] = (nat.win_layout(rand_bits, 16)[0] - 1) * nmul  # k_djn_pub_nd at window 16
+    s, m = sliding_window_ops(n)
+    out["encrypt_public_nodjn_per_s"] = s * nsq + m * nmul  # k_ndig_pow_n: r^n
+    ep, eq = n % (p * (p - 1)), n % (q * (q - 1))
+    sp, mp = sliding_window_ops(ep)
+    sq_, mq = sliding_window_ops(eq)
+    out["encrypt_private_nodjn_per_s"] = (sp + sq_) * dsq + (mp + mq) * dmul  # k_dec_pmd_pow with e_P
+    out["scalar_mul_53bit_per_s"] = 53 * nsq + 26 * nmul  # k_ndig_pow_k: 4-bit windows, table x^2..x^15
+    return out
+
+
+def model_macs(bits, key_material, win_bits):
+    """SURVEY 8(d)'s 32-bit CIOS model per operation (2 s^2 + s MACs per
+    product, s = K/32 words per prime, 2 s per n^2): what roofline.achieved
+    uses for the headline"""
+    if bits != 2048:
+        return {}
+    p, q, n, _ = key_material
+    from xfl_amd import _native as nat
+    s1, s2 = 64, 128
+    prod1, prod2 = 2 * s1 * s1 + s1, 2 * s2 * s2 + s2
+    nwin = nat.win_layout(n.bit_length() // 2, win_bits)[0]
+    vb = lambda e: e.bit_length() + -(-e.bit_length() // 5) + 16  # noqa: E731  variable-base window-5 products
+    ep, eq = n % (p * (p - 1)), n % (q * (q - 1))
+    return {"headline": 2 * nwin * prod1, "decrypt_per_s": (vb(p - 1) + vb(q - 1)) * prod1, "add_per_s": prod2,
+            "sum_per_s": prod2, "encrypt_public_djn_per_s": nat.win_layout(n.bit_length() // 2, 16)[0] * prod2,
+            "encrypt_public_nodjn_per_s": vb(n) * prod2, "encrypt_private_nodjn_per_s": (vb(ep) + vb(eq)) * prod1,
+            "scalar_mul_53bit_per_s": (53 + 11 + 16) * prod2}
+
+
+def issued_fractions(ops, bits, key_material, win_bits, headline_rate, clock_ghz):
+    """ops["issued"]: per operation the schedule's mads x the measured rate
+    over the v_mad_u64_u32 issue peak (16,384 lanes x clock: 2.4 GHz, and
+    the clock the counter passes measured under this load), next to the
+    8(d) model fraction (VERDICT r5 #7)"""
+    mads, model = issued_mads(bits, key_material, win_bits), model_macs(bits, key_material, win_bits)
+    rates = dict(ops)
+    rates["headline"] = headline_rate
+    out = {}
+    for k, v in mads.items():
+        r = rates.get(k)
+        if not r:
+            continue
+        rec = {"mads_per_op": v, "model_macs_per_op": model.get(k), "rate_per_s": r,
+               "issued_mad_frac": v * r / PEAK_MAC_PER_S, "model_frac": model.get(k, 0) * r / PEAK_MAC_PER_S}
+        if clock_ghz:
+            rec["issued_mad_frac_at_clock"] = v * r / (16384 * clock_ghz * 1e9)
+        out[k] = rec
+    return out
+
+
 def _timed(fn, reps=3):
     """Average seconds per call of fn() on the current stream (1 untimed warm call)."""
     import torch
@@ -674,6 +790,10 @@ def main():
             rec["config"]["proxy_world"] = pipe.proxy
             rec["config"]["proxy_gather_bytes_per_step"] = (pipe.proxy - world) * N * dk.n2w * 4
             rec["config"]["gather_target_bytes"] = sum(g.numel() * 4 for g in pipe.gathered)
+        hm = issued_mads(bits, (p, q, n, h), args.win).get("headline")
+        if hm:  # the kernel's own schedule (digit products), not the 8(d) model
+            rec["roofline"]["issued_mads_per_element"] = hm
+            rec["roofline"]["issued_mad_frac"] = N * hm / pow_avg_s / PEAK_MAC_PER_S
         if pmc and pmc.get("clock_ghz"):
             # the counter pass's clock under this load (SQ_BUSY_CYCLES) and VALU
             # busy: `peak` is the 2.4 GHz figure, the kernel runs below it
@@ -693,6 +813,8 @@ def main():
             gc.collect()
             torch.cuda.empty_cache()
             rec["ops"].update(measure_dropin(nat, dev, bits, xh, (p, q, n, h)))
+            clock = float(pmc["clock_ghz"]) if pmc and pmc.get("clock_ghz") else None
+            rec["ops"]["issued"] = issued_fractions(rec["ops"], bits, (p, q, n, h), args.win, N / pow_avg_s, clock)
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baselines(bits, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

@@ -136,6 +136,13 @@ int xhe_scatter_rows(const uint32_t* src_dev, const int64_t* idx_dev, int64_t co
  * words, n2w <= 1023): the per-element input of xhe_wire_layout, so the
  * serialize payload is sized before the ciphertexts are downloaded. */
 int xhe_row_bits(const uint32_t* words_dev, int64_t count, int n2w, int16_t* bits_dev, void* stream);
+/* Host only (no device): the constant blocks k_dec_rns reads for the prime P
+ * (p_words: pw words) - the bases' block (shared_out: XHE_RNS_SHARED_WORDS)
+ * and P's block (prime_out: XHE_RNS_PRIME_WORDS); for tests against
+ * tools/rns_model.py. */
+#define XHE_RNS_SHARED_WORDS 26696
+#define XHE_RNS_PRIME_WORDS 2056
+int xhe_rns_constants(const uint32_t* p_words, int pw, uint32_t* shared_out, uint32_t* prime_out);
 
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
 int xhe_multiexp_host(const xhe_key* key, const uint32_t* bases, int64_t nbases, const int32_t* idx, const uint32_t* k,

@@ -172,6 +172,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--keys", type=int, default=2)
     ap.add_argument("--products", type=int, default=300)
+    ap.add_argument("--ops", action="store_true", help="also check the kernel's channel arithmetic")
     args = ap.parse_args()
     rng = random.Random(5)
     print(f"K={K} moduli of {W} bits per base: M ~ 2^{M.bit_length()}, M' ~ 2^{M2.bit_length()}")
@@ -197,3 +198,40 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# ---- the kernel's channel arithmetic (32-bit registers), checked exhaustively
+# at the edges and on random operands for every modulus
+U32 = (1 << 32) - 1
+
+
+def k_red(x, m, mu):
+    """x < 2^59 -> x mod m: q = mulhi(x >> 27, mu), r = lo32(x) - q m, three min-corrections"""
+    assert x < 1 << 59
+    q = ((x >> 27) * mu) >> 32
+    r = (x - q * m) & U32
+    for _ in range(3):
+        r = min(r, (r - m) & U32)
+    return r
+
+
+def k_red64(x, m, mu, t32):
+    """x < 2^63 (the 74-term column sums): fold the high word by 2^32 mod m first"""
+    assert x < 1 << 63
+    return k_red((x >> 32) * t32 + (x & U32), m, mu)
+
+
+def check_channel_ops(rng, n=20000):
+    for m in B + B2:
+        mu = (1 << 59) // m
+        assert (1 << 31) < mu < (1 << 32)
+        t32 = (1 << 32) % m
+        for x in [0, 1, m - 1, m, (m - 1) ** 2, (1 << 59) - 1] + [rng.randrange(1 << 59) for _ in range(n // 100)]:
+            assert k_red(x, m, mu) == x % m, (m, x)
+        for x in [(1 << 63) - 1, 74 * (m - 1) ** 2] + [rng.randrange(1 << 63) for _ in range(n // 100)]:
+            assert k_red64(x, m, mu, t32) == x % m, (m, x)
+    print("channel arithmetic: Barrett reductions exact for every modulus")
+
+
+if __name__ == "__main__" and "--ops" in __import__("sys").argv:
+    check_channel_ops(random.Random(9))

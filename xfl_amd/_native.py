@@ -71,6 +71,7 @@ SIGNATURES = {
     "xhe_wire_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
                                      ctypes.c_int, _vp, ctypes.c_int64]),
     "xhe_row_bits": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
+    "xhe_rns_constants": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64), _vp, ctypes.POINTER(ctypes.c_int)]),
     "xhe_host_prefault": (ctypes.c_int, [_vp, ctypes.c_int64]),

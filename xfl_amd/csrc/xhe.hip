@@ -21,6 +21,7 @@
 #include "xhe_kernels.hpp"
 #include "dec_wave.hpp"
 #include "barrett_dev.hpp"
+#include "rns_dev.hpp"
 
 using namespace xhe;
 
@@ -162,6 +163,188 @@ struct Blob {
     return put(v);
   }
 };
+
+// ---- RNS small-batch decrypt constants (rns_dev.hpp k_dec_rns; checked
+// against tools/rns_model.py, which builds the same bases)
+namespace rnsh {
+inline bool prime32(uint32_t n) {  // deterministic Miller-Rabin for n < 2^32
+  if (n < 2) return false;
+  for (uint32_t p : {2u, 3u, 5u, 7u})
+    if (n % p == 0) return n == p;
+  uint32_t d = n - 1;
+  int r = 0;
+  while (!(d & 1)) d >>= 1, ++r;
+  for (uint64_t a : {2ull, 3ull, 5ull, 7ull}) {
+    uint64_t x = 1, b = a, e = d;
+    while (e) {
+      if (e & 1) x = x * b % n;
+      b = b * b % n;
+      e >>= 1;
+    }
+    if (x == 1 || x == n - 1) continue;
+    bool ok = false;
+    for (int i = 1; i < r && !ok; ++i) {
+      x = x * x % n;
+      ok = x == n - 1;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+inline uint32_t inv_mod(uint32_t a, uint32_t m) {  // a^-1 mod m (gcd = 1)
+  int64_t t0 = 0, t1 = 1, r0 = m, r1 = a % m;
+  while (r1) {
+    const int64_t q = r0 / r1;
+    std::swap(r0, r1);
+    r1 -= q * r0;
+    std::swap(t0, t1);
+    t1 -= q * t0;
+  }
+  return (uint32_t)((t0 % (int64_t)m + m) % m);
+}
+inline uint32_t inv_2_32(uint32_t a) {  // odd a
+  uint32_t x = a;
+  for (int i = 0; i < 5; ++i) x *= 2u - a * x;
+  return x;
+}
+inline uint32_t mod_small(const BigU& x, uint32_t m) {  // m = 0: mod 2^32
+  if (m == 0) return x.word(0);
+  uint64_t r = 0;
+  for (size_t k = x.w.size(); k-- > 0;) r = ((r << 32) | x.w[k]) % m;
+  return (uint32_t)r;
+}
+struct Bases {
+  std::vector<uint32_t> b, b2;  // B and B' (the 2 RK largest primes below 2^28, interleaved)
+  BigU M, M2;
+  std::vector<BigU> Mi, M2j;
+  std::vector<uint32_t> shared;  // the S_* block
+};
+inline const Bases& bases() {
+  static const Bases B = [] {
+    using namespace rns;
+    Bases r;
+    std::vector<uint32_t> pr;
+    for (uint32_t c = (1u << 28) - 1; (int)pr.size() < 2 * RK; c -= 2)
+      if (prime32(c)) pr.push_back(c);
+    for (int i = 0; i < 2 * RK; ++i) (i % 2 ? r.b2 : r.b).push_back(pr[i]);
+    r.M = BigU(1);
+    r.M2 = BigU(1);
+    for (int i = 0; i < RK; ++i) {
+      r.M = mul(r.M, BigU(r.b[i]));
+      r.M2 = mul(r.M2, BigU(r.b2[i]));
+    }
+    for (int i = 0; i < RK; ++i) {
+      BigU q;
+      divmod(r.M, BigU(r.b[i]), &q, nullptr);
+      r.Mi.push_back(q);
+      divmod(r.M2, BigU(r.b2[i]), &q, nullptr);
+      r.M2j.push_back(q);
+    }
+    std::vector<uint32_t>& s = r.shared;
+    s.assign(S_WORDS, 0u);
+    for (int t = 0; t < NT; ++t) {
+      const bool gB = t < 128;
+      const int ch = gB ? t : t - 128;
+      const bool isr = t == RLANE;
+      if (!(ch < RK || isr)) continue;
+      const uint32_t m = isr ? 0u : (gB ? r.b[ch] : r.b2[ch]);
+      if (m) {
+        s[S_M + t] = m;
+        s[S_MU + t] = (uint32_t)((1ull << 59) / m);
+        s[S_T32 + t] = (uint32_t)((1ull << 32) % m);
+      }
+      for (int i = 0; i < RK; ++i)  // B: |M'_j|_(m_i); B': |M_i|_(m'_j); 2^32: |M_i|_(2^32)
+        s[S_ROWS + i * NT + t] = gB ? mod_small(r.M2j[i], m) : mod_small(r.Mi[i], m);
+      if (gB) {
+        s[S_B + t] = mod_small(r.M2, m);                       // |M'|_(m_i)
+        s[S_C + t] = inv_mod(mod_small(r.Mi[ch], m), m);        // |M_i^-1|_(m_i)
+      } else if (!isr) {
+        const uint64_t minv = inv_mod(mod_small(r.M, m), m);
+        s[S_B + t] = (uint32_t)minv;                                                   // |M^-1|_(m'_j)
+        s[S_C + t] = (uint32_t)(minv * inv_mod(mod_small(r.M2j[ch], m), m) % m);     // |M^-1 M'_j^-1|_(m'_j)
+        s[S_D + t] = r.M2j[ch].word(0);                         // |M'_j|_(2^32)
+      } else {
+        s[S_B + t] = inv_2_32(r.M.word(0));                     // M^-1 mod 2^32
+      }
+    }
+    for (int i = 0; i < RK; ++i) {
+      const std::vector<uint32_t> l = r.Mi[i].to_limbs(28, RKP);
+      for (int c = 0; c < RKP; ++c) s[S_MPOS + i * RKP + c] = l[c];
+    }
+    const std::vector<uint32_t> lm = r.M.to_limbs(28, RKP);
+    for (int c = 0; c < RKP; ++c) s[S_MFULL + c] = lm[c];
+    s[S_M2RINV] = inv_2_32(r.M2.word(0));
+    return r;
+  }();
+  return B;
+}
+// the per-prime block for N = P^2: |-N^-1 M_i^-1| (B), |N M^-1| and |N M^-1
+// M'_j^-1| (B'), N mod 2^32; M^3 mod N in every channel; and the exponent P - 1
+// as the kernel's sliding-window schedule (5-bit windows, the rule of
+// pow_uniform_exp: each window ends in a set bit)
+inline std::vector<uint32_t> prime_block(const BigU& P) {
+  using namespace rns;
+  const Bases& b = bases();
+  const BigU N = mul(P, P);
+  std::vector<uint32_t> v(P_WORDS, 0u);
+  const BigU MN = mod(b.M, N);
+  const BigU M3 = mulmod(mulmod(MN, MN, N), MN, N);
+  for (int t = 0; t < NT; ++t) {
+    const bool gB = t < 128;
+    const int ch = gB ? t : t - 128;
+    const bool isr = t == RLANE;
+    if (!(ch < RK || isr)) continue;
+    const uint32_t m = isr ? 0u : (gB ? b.b[ch] : b.b2[ch]);
+    if (gB) {
+      const uint64_t ni = inv_mod(mod_small(N, m), m), mi = inv_mod(mod_small(b.Mi[ch], m), m);
+      v[P_A + t] = (uint32_t)((m - ni * mi % m) % m);
+    } else if (!isr) {
+      const uint64_t nm = (uint64_t)mod_small(N, m) * inv_mod(mod_small(b.M, m), m) % m;
+      v[P_A + t] = (uint32_t)nm;
+      v[P_A2 + t] = (uint32_t)(nm * inv_mod(mod_small(b.M2j[ch], m), m) % m);
+    } else {
+      v[P_A + t] = N.word(0);
+    }
+    v[P_M3 + t] = mod_small(M3, m);
+  }
+  // schedule over e = P - 1 (bits high to low)
+  const BigU e = sub(P, BigU(1));
+  const int nb = (int)e.bits();
+  auto bit = [&](int i) { return (e.word((size_t)i / 32) >> (i % 32)) & 1u; };  // i: from the bottom
+  auto window = [&](int hi, int* lo_out) {  // the window from bit hi down (at most 5 bits, ends in a set bit)
+    int lo = std::max(hi - 4, 0);
+    while (!bit(lo)) ++lo;
+    uint32_t val = 0;
+    for (int i = hi; i >= lo; --i) val = val << 1 | bit(i);
+    *lo_out = lo;
+    return val;
+  };
+  int ns = 0, lo;
+  const uint32_t first = window(nb - 1, &lo);
+  v[P_SCHED + ns++] = (first - 1) / 2;
+  int i = lo - 1;
+  uint32_t sq = 0;
+  while (i >= 0) {
+    if (!bit(i)) {
+      ++sq;
+      --i;
+      continue;
+    }
+    const uint32_t w = window(i, &lo);
+    sq += (uint32_t)(i - lo + 1);
+    if (ns >= P_SCHED_MAX) throw std::runtime_error("rns schedule overflow");
+    v[P_SCHED + ns++] = sq << 8 | ((w - 1) / 2 + 1);
+    sq = 0;
+    i = lo - 1;
+  }
+  if (sq) {
+    if (ns >= P_SCHED_MAX) throw std::runtime_error("rns schedule overflow");
+    v[P_SCHED + ns++] = sq << 8;
+  }
+  v[P_NS] = (uint32_t)ns;
+  return v;
+}
+}  // namespace rnsh
 
 struct ModOff {
   size_t N, R1, R2, R3, Rpow = 0;
@@ -417,6 +600,7 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     size_t ep = 0, eq = 0;
     size_t topc_p = 0, topc_q = 0;
     size_t nprime_p2 = 0, nprime_q2 = 0;
+    size_t rns = 0, rns_p = 0, rns_q = 0;
     ModOff xd[2];
     size_t xkn2[2] = {0, 0}, xrmn[2] = {0, 0}, xtopc[2] = {0, 0}, xfold[2] = {0, 0}, xdwt[2] = {0, 0};
     size_t xdw[2] = {0, 0}, xhpR[2] = {0, 0};
@@ -437,6 +621,10 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
       const BigU R = pow2((size_t)s2.W * s2.S);
       o.nprime_p2 = bl.put_limbs(sub(R, modinv(p2, R)), s2);
       o.nprime_q2 = bl.put_limbs(sub(R, modinv(q2, R)), s2);
+      // the RNS decrypt's bases (shared by every key) and per-prime constants
+      o.rns = bl.put(rnsh::bases().shared);
+      o.rns_p = bl.put(rnsh::prime_block(P));
+      o.rns_q = bl.put(rnsh::prime_block(Q));
     }
     BigU R2p = pow2((size_t)s2.W * s2.S);
     BigU Rp2 = mod(R2p, p2), Rq2 = mod(R2p, q2);
@@ -648,6 +836,9 @@ void key_create_impl(xhe_key* k, const BigU& n, const BigU* p, const BigU* q, co
     if (K == 2048) {
       kd.p2_nprime = B + o.nprime_p2;
       kd.q2_nprime = B + o.nprime_q2;
+      kd.rns = B + o.rns;
+      kd.rns_p = B + o.rns_p;
+      kd.rns_q = B + o.rns_q;
     }
 #if XHE_PMD && XHE_LDS_ROWS
     if (K == 2048) {
@@ -1821,6 +2012,16 @@ void dec_pmdx_launch(const xhe_key* k, const uint32_t* ct, int64_t n, int64_t ch
 }
 #endif
 
+// $XHE_DEC_RNS=0: the small-batch 2048-bit decrypt on k_dec_wave (the
+// WaveMont product) instead of k_dec_rns (A/B measurement)
+bool dec_rns_on() {
+  static const bool on = [] {
+    const char* e = getenv("XHE_DEC_RNS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class Sh>
 void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t* m, hipStream_t s) {
   using MP2 = typename Sh::MP2;
@@ -1857,11 +2058,16 @@ void decrypt_impl(const xhe_key* k, const uint32_t* ct, int64_t count, uint32_t*
 #endif
     if (tpi == 64) {
       if constexpr (wave_ok) {
-        {
-        static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave shares the MP2 limbs");
-        ProfScope ps("k_dec_wave", s);
-        hipLaunchKernelGGL((k_dec_wave<74, XHE_DEC_NWV>), dim3((unsigned)n, 2), dim3(64 * XHE_DEC_NWV), 0, s, k->kd, cto, n, (int)MP2::S4, xrows);
-        HIPCHK(hipGetLastError());
+        static_assert(MP2::S == 74 && MP2::W == 28, "k_dec_wave / k_dec_rns share the MP2 limbs");
+        if (k->kd.rns && dec_rns_on()) {
+          ProfScope ps("k_dec_rns", s);
+          hipLaunchKernelGGL(k_dec_rns, dim3((unsigned)n, 2), dim3(rns::NT), 0, s, k->kd, cto, n, (int)MP2::S4, xrows);
+          HIPCHK(hipGetLastError());
+        } else {
+          ProfScope ps("k_dec_wave", s);
+          hipLaunchKernelGGL((k_dec_wave<74, XHE_DEC_NWV>), dim3((unsigned)n, 2), dim3(64 * XHE_DEC_NWV), 0, s, k->kd,
+                             cto, n, (int)MP2::S4, xrows);
+          HIPCHK(hipGetLastError());
         }
       }
     } else if (tpi == 16) dec_pow_launch<typename Sh::MP2X, 2, MP2>(k, cto, n, chunk, xrows, s);
@@ -2259,6 +2465,19 @@ __global__ void k_row_bits(const uint32_t* __restrict__ w, int64_t count, int n2
 }
 
 extern "C" {
+
+int xhe_rns_constants(const uint32_t* p_words, int pw, uint32_t* shared_out, uint32_t* prime_out) {
+  return guarded([&]() -> int {
+    if (!p_words || pw <= 0 || !shared_out || !prime_out) return fail(XHE_EINVAL, "xhe_rns_constants: bad argument");
+    const BigU P = BigU::from_words(p_words, (size_t)pw);
+    if (P.bits() > 1024 || P.bits() < 2) return fail(XHE_EINVAL, "xhe_rns_constants: P must have 2..1024 bits");
+    const std::vector<uint32_t>& sh = rnsh::bases().shared;
+    std::copy(sh.begin(), sh.end(), shared_out);
+    const std::vector<uint32_t> pb = rnsh::prime_block(P);
+    std::copy(pb.begin(), pb.end(), prime_out);
+    return XHE_OK;
+  });
+}
 
 int xhe_row_bits(const uint32_t* words_dev, int64_t count, int n2w, int16_t* bits_dev, void* stream) {
   return guarded([&]() -> int {

@@ -108,6 +108,9 @@ struct KeyDev {
   // ---- one-wave decrypt exponentiation (k_dec_wave, 2048-bit keys): the
   // full Montgomery inverse -P^-2 mod R of the MP2 shape (R = 2^(28*74))
   const uint32_t *p2_nprime, *q2_nprime;
+  // ---- RNS small-batch decrypt (k_dec_rns, rns_dev.hpp; 2048-bit private
+  // keys): the bases' constant block and one block per prime (null: off)
+  const uint32_t *rns, *rns_p, *rns_q;
   // ---- one-block Horner of the mat-vec mod n^2 (k_mexp_horner_wave, 2048-bit
   // keys): n^2 in 154 limbs of 27 bits (R_w = 2^4158), -n^-2 mod R_w and
   // C = R_w^2 R_X^-1 mod n^2 (R_X = 2^(27*160): the 16-lane shape's R)
