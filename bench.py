@@ -438,7 +438,7 @@ def measure_dropin(nat, device, key_bits, xh, key_material):
     out["dropin_deserialize_per_s"] = nh / t
     back = Paillier.decrypt(ctx, Paillier.ciphertext_from(None, wire[False], compression=False))
     out["dropin_roundtrip_max_abs_err"] = float(np.max(np.abs(back - x32)))
-    t = _timed(lambda: enc_ser(True), reps=1)
+    t = _timed(lambda: enc_ser(True), reps=2)
     out["dropin_encrypt_serialize_zstd_per_s"] = nh / t
     note("dropin_encrypt_serialize_zstd_per_s")
     out["wire_bytes_per_ciphertext"] = len(wire[False]) / nh
@@ -467,6 +467,9 @@ def measure_dropin(nat, device, key_bits, xh, key_material):
     back = Paillier.decrypt(ctx, enc[0])
     out["dropin_encrypt_steady_max_abs_err"] = float(np.max(np.abs(back - x32)))
     out["dropin_encrypt_steady_ok"] = bool(np.allclose(back, x32, rtol=1e-6, atol=1e-7))
+    # the label trainer's encrypt -> serialize(compression=True) at that window
+    out["dropin_encrypt_serialize_zstd_steady_per_s"] = nh / _timed(lambda: enc_ser(True), reps=2)
+    win["dropin_encrypt_serialize_zstd_steady_per_s"] = ctx._dev[device].win_bits
     out["dropin_table_bytes_steady"] = nat.table_bytes(key_bits, ctx._dev[device].win_bits)
     out["dropin_window_bits"] = win
     wire.clear()

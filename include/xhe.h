@@ -140,8 +140,8 @@ int xhe_row_bits(const uint32_t* words_dev, int64_t count, int n2w, int16_t* bit
  * (p_words: pw words) - the bases' block (shared_out: XHE_RNS_SHARED_WORDS)
  * and P's block (prime_out: XHE_RNS_PRIME_WORDS); for tests against
  * tools/rns_model.py. */
-#define XHE_RNS_SHARED_WORDS 26696
-#define XHE_RNS_PRIME_WORDS 2056
+#define XHE_RNS_SHARED_WORDS 19784
+#define XHE_RNS_PRIME_WORDS 2088
 int xhe_rns_constants(const uint32_t* p_words, int pw, uint32_t* shared_out, uint32_t* prime_out);
 
 /* Host-buffer variants (H2D -> kernels -> D2H on an internal stream). */
@@ -202,6 +202,20 @@ int xhe_wire_layout(const int16_t* bits, const int32_t* exps, int64_t count, int
                     int framed, int64_t* elem_off, uint8_t* out, int64_t cap, int64_t* out_len);
 int xhe_wire_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
                   const int64_t* elem_off, int framed, uint8_t* out, int64_t cap);
+/* The layout range by range, for bit lengths that arrive chunk by chunk
+ * too (a serialize that starts while the encryption runs): begin sets
+ * elem_off[0] and *max_len = the payload size if every element had the
+ * largest bit length n2w words allow (allocate that), and with out writes the
+ * header; layout_part fills elem_off[lo+1..hi] from elem_off[lo] and the bit
+ * lengths of elements lo..hi-1 (bits[0] = element lo); rows as above, for
+ * ranges laid out so far; finish writes the footer and, framed, the zstd frame
+ * and block headers, and sets *out_len = the payload's real size (the caller
+ * cuts its buffer to it). The bytes equal xhe_wire_encode_frame's. */
+int xhe_wire_begin(const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim, int framed,
+                   int64_t* elem_off, int64_t* max_len, uint8_t* out, int64_t cap);
+int xhe_wire_layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                         int64_t* elem_off);
+int xhe_wire_finish(int64_t count, const int64_t* elem_off, int framed, uint8_t* out, int64_t cap, int64_t* out_len);
 
 /* A zstd frame (RFC 8878, one frame, content size in the header) holding
  * src[0..n) as raw blocks, written by several host threads: what

@@ -193,6 +193,24 @@ static void own_format(std::mt19937_64& rng) {
             std::abort();
         }
         if (piece != out) std::abort();
+        {  // the same range by range (the pipeline over a running encryption):
+           // header, per-range offsets from the previous range's end, rows, footer
+          std::vector<int64_t> o2((size_t)count + 1, -1);
+          Bytes inc((size_t)need + 4096, 0xEE);  // over-allocated, as the caller does
+          const xhe::wire::Sink is{inc.data(), 0};
+          o2[0] = xhe::wire::head_bytes(shape, 2);
+          xhe::wire::write_head(shape, 2, is);
+          for (int64_t lo = 0; lo < count; lo += 1000) {
+            const int64_t hi = std::min<int64_t>(count, lo + 1000);
+            xhe::wire::layout_part(bits.data() + lo, ex.data(), lo, hi, count, n2w, o2.data());
+            if (!xhe::wire::write_rows(ct.data() + (size_t)lo * n2w, ex.data(), lo, hi, count, n2w, o2.data(), is,
+                                       threads))
+              std::abort();
+          }
+          xhe::wire::write_foot(o2[count], is);
+          if (o2[count] + 3 != need || o2 != offs) std::abort();
+          if (std::memcmp(inc.data(), out.data(), (size_t)need)) std::abort();
+        }
         if (count > 1) {  // a wrong bit length is refused
           bits[1] = (int16_t)(bits[1] > 8 ? bits[1] - 8 : bits[1] + 8);
           xhe::wire::layout(bits.data(), ex.data(), count, n2w, shape, 2, offs.data(), nullptr, threads);

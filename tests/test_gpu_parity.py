@@ -102,10 +102,10 @@ def test_host_encrypt_chunking_is_invisible():
 
 
 @pytest.mark.parametrize("fx", FIXTURES)
-@pytest.mark.parametrize("count", [1, 300, 600, 5000, 20000, 30000])
+@pytest.mark.parametrize("count", [1, 300, 1024, 1100, 5000, 20000, 30000])
 def test_decrypt_shapes_bit_exact(fx, count):
     """The decrypt exponentiation runs in four lane shapes chosen by batch
-    size (2048-bit keys: a 4-wave block per residue up to 512 elements, then
+    size (2048-bit keys: a block per residue in RNS form up to 1,024 elements, then
     16 lanes per residue up to 5,120, 4 up to 28,672, then 1): the golden
     ciphertexts tiled to each regime decrypt to the golden m."""
     from xfl_amd._native import ints_to_words, words_to_ints
@@ -122,7 +122,7 @@ def test_decrypt_shapes_bit_exact(fx, count):
     assert out == (ms * reps)[:count]
 
 
-@pytest.mark.parametrize("count", [7, 300, 700])
+@pytest.mark.parametrize("count", [7, 300, 700, 1500])
 def test_decrypt_arbitrary_residues(count):
     """Any c < n^2 coprime to n (as every ciphertext is), not only
     well-formed ciphertexts, decrypts as the reference's arithmetic does

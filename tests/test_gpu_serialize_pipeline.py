@@ -64,3 +64,28 @@ def test_async_encrypt_raises_and_decrypts():
     bad[77777] = np.nan
     with pytest.raises(ValueError):
         Paillier.encrypt(ctx, bad, precision=7)
+
+
+def test_pipeline_over_running_encryption_and_in_place_writes():
+    """An encryption launched in ENC_SUB-row pieces on two streams (each
+    marked by an event) serializes while it runs - the copy stream waits per
+    chunk only for the launches that write its rows - and the bytes equal the
+    two-step path; rows rewritten in place afterwards (an obfuscated view,
+    resident.put_rows) drop the marks, so the next serialize sees them."""
+    from xfl_amd.paillier import Paillier
+    from xfl_amd.paillier import wire
+    ctx = _ctx()
+    rng = np.random.default_rng(6)
+    n = 2 * wire.ENC_SUB + 3 * wire.PIPE_CHUNK + 77
+    x = rng.standard_normal(n).astype(np.float32)
+    enc = Paillier.encrypt(ctx, x, precision=7)
+    assert len(enc._st.d._xhe_ready) == -(-n // wire.ENC_SUB)
+    got = Paillier.serialize(enc, compression=True)
+    assert got == wire.encode_words(enc.words, enc.exponents, enc.shape, compression=True)
+    enc2 = Paillier.encrypt(ctx, x, precision=7)
+    Paillier.obfuscate(enc2[1000:2000])
+    assert not hasattr(enc2._st.d, "_xhe_ready")
+    enc2._st.h = None
+    got2 = Paillier.serialize(enc2, compression=False)
+    assert got2 == wire.encode_words(enc2.words, enc2.exponents, enc2.shape)
+    assert np.allclose(Paillier.decrypt(ctx, enc2), x, atol=1e-6)

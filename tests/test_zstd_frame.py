@@ -90,3 +90,51 @@ def test_serialize_compressed_roundtrip_large_array():
     assert plain == Paillier.serialize(arr, compression=False)
     back = Paillier.ciphertext_from(None, blob, compression=True)
     assert np.array_equal(back.words, w) and np.array_equal(back.exponents, e)
+
+
+@pytest.mark.parametrize("framed", [False, True])
+def test_incremental_layout_equals_one_pass(framed):
+    """The serialize pipeline's range-by-range layout (xhe_wire_begin /
+    layout_part / rows / finish over a payload allocated at the largest size
+    the elements could need, then cut in place by shrink_bytes) gives the
+    bytes of the one-pass writer (xhe_wire_encode_frame), for ranges that
+    cross APPENDS batches and zstd block borders."""
+    from xfl_amd.paillier import wire
+    rng = np.random.default_rng(8)
+    count, n2w = 5003, 128
+    ct = rng.integers(0, 2 ** 32, (count, n2w), dtype=np.uint64).astype(np.uint32)
+    ct[:, -1] >>= rng.integers(0, 32, count).astype(np.uint32)  # ragged bit lengths
+    ct[7] = 0
+    ex = rng.integers(-3, 400, count).astype(np.int32)
+    shape = (count,)
+    want = wire.encode_words(ct, ex, shape)
+    if framed:
+        want = compat.compress(want) if len(want) < compat.RAW_FRAME_MIN else wire.encode_words(ct, ex, shape, True)
+    L = nat.lib()
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    shp = np.array(shape, np.int64)
+    off = np.empty(count + 1, np.int64)
+    mx = ctypes.c_int64()
+    nat.check(L.xhe_wire_begin(vp(ex), count, n2w, vp(shp), 1, int(framed), vp(off), ctypes.byref(mx), None, 0))
+    out = nat.alloc_bytes(mx.value)
+    optr = ctypes.c_void_p(ctypes.cast(out, ctypes.c_void_p).value)
+    nat.check(L.xhe_wire_begin(vp(ex), count, n2w, vp(shp), 1, int(framed), vp(off), ctypes.byref(mx), optr, mx.value))
+    bits = np.array([0 if not r.any() else 32 * int(np.nonzero(r)[0][-1]) + int(r[np.nonzero(r)[0][-1]]).bit_length()
+                     for r in ct], np.int16)
+    for lo in range(0, count, 1234):
+        hi = min(count, lo + 1234)
+        b = np.ascontiguousarray(bits[lo:hi])
+        nat.check(L.xhe_wire_layout_part(vp(b), vp(ex), lo, hi, count, n2w, vp(off)))
+        rows = np.ascontiguousarray(ct[lo:hi])
+        nat.check(L.xhe_wire_rows(vp(rows), vp(ex), lo, hi, count, n2w, vp(off), int(framed), optr, mx.value))
+    size = ctypes.c_int64()
+    nat.check(L.xhe_wire_finish(count, vp(off), int(framed), optr, mx.value, ctypes.byref(size)))
+    assert size.value <= mx.value
+    box = [out]
+    del out
+    got = nat.shrink_bytes(box, size.value)
+    if framed and len(wire.encode_words(ct, ex, shape)) >= compat.RAW_FRAME_MIN:
+        assert got == want
+    elif not framed:
+        assert got == want
+    assert compat.decompress(got) == wire.encode_words(ct, ex, shape) if framed else True

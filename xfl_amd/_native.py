@@ -7,6 +7,7 @@ fallback: if the library or a GPU is missing, every entry point raises.
 import ctypes
 import mmap
 import os
+import sys
 import threading
 import weakref
 
@@ -70,6 +71,12 @@ SIGNATURES = {
                                        _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "xhe_wire_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
                                      ctypes.c_int, _vp, ctypes.c_int64]),
+    "xhe_wire_begin": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, _vp,
+                                      ctypes.POINTER(ctypes.c_int64), _vp, ctypes.c_int64]),
+    "xhe_wire_layout_part": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                            _vp]),
+    "xhe_wire_finish": (ctypes.c_int, [ctypes.c_int64, _vp, ctypes.c_int, _vp, ctypes.c_int64,
+                                       ctypes.POINTER(ctypes.c_int64)]),
     "xhe_row_bits": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),
     "xhe_rns_constants": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     "xhe_wire_decode": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
@@ -186,6 +193,38 @@ def _pybytes(n):
     f.restype = ctypes.py_object
     f.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
     return f(None, n)
+
+
+def shrink_bytes(box, n):
+    """box: a one-element list holding the only reference to a bytes object
+    (from alloc_bytes); returns that object cut to its first n bytes in place
+    (_PyBytes_Resize: a realloc that keeps the block, no copy) - the
+    serialize pipeline allocates the largest payload its elements could need
+    before their sizes are known. Falls back to a copy when anything else
+    still refers to the object."""
+    b = box.pop()
+    n = int(n)
+    if n == len(b):
+        return b
+    if not 2 <= n < len(b):
+        raise ValueError("shrink_bytes: n must be in [2, len)")
+    if sys.getrefcount(b) != 2:  # b + getrefcount's argument
+        return b[:n]
+    api = ctypes.pythonapi
+    api.Py_IncRef.argtypes = [ctypes.c_void_p]
+    api.Py_DecRef.argtypes = [ctypes.c_void_p]
+    api.Py_NewRef.argtypes = [ctypes.c_void_p]
+    api.Py_NewRef.restype = ctypes.py_object
+    api._PyBytes_Resize.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_ssize_t]
+    api._PyBytes_Resize.restype = ctypes.c_int
+    slot = ctypes.c_void_p(id(b))
+    api.Py_IncRef(slot.value)  # the slot's own reference, the only one after del
+    del b
+    if api._PyBytes_Resize(ctypes.byref(slot), n) != 0:  # (the object is gone then)
+        raise MemoryError("shrink_bytes: _PyBytes_Resize failed")
+    out = api.Py_NewRef(slot.value)
+    api.Py_DecRef(slot.value)
+    return out
 
 
 def alloc_bytes(n):

@@ -25,7 +25,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libxhe.so")
 OBJ = os.path.join(HERE, "lib", "obj")
 HEADER = os.path.join(ROOT, "include", "xhe.h")
-DEVICE_DEPS = [os.path.join(CSRC, f) for f in ("xhe.hip", "xhe_kernels.hpp", "bn_dev.hpp", "pdigit_dev.hpp", "dec_wave.hpp", "barrett_dev.hpp", "hostbn.hpp",
+DEVICE_DEPS = [os.path.join(CSRC, f) for f in ("xhe.hip", "xhe_kernels.hpp", "bn_dev.hpp", "pdigit_dev.hpp", "dec_wave.hpp", "barrett_dev.hpp", "rns_dev.hpp", "hostbn.hpp",
                                                "abi_common.hpp")] + [HEADER]
 HOST_DEPS = [os.path.join(CSRC, f) for f in ("wire_abi.cpp", "wire.hpp", "abi_common.hpp")] + [HEADER]
 SOURCES = sorted(set(DEVICE_DEPS + HOST_DEPS))

@@ -434,6 +434,35 @@ inline int64_t layout(const int16_t* bits, const int32_t* exps, int64_t count, i
   return total;
 }
 
+// ---- the same layout element range by element range, for words whose bit
+// lengths arrive chunk by chunk too (an encryption still running when the
+// serialize starts): the header's size first (off[0]), then each range's
+// offsets from the offset its first element starts at, the footer last.
+inline int64_t head_bytes(const int64_t* shape, int ndim) {
+  Writer hw{nullptr, 0};
+  emit_header(hw, shape, ndim);
+  return hw.n;
+}
+inline void write_head(const int64_t* shape, int ndim, const Sink& sink) {
+  const int64_t head = head_bytes(shape, ndim);
+  std::vector<uint8_t> hb((size_t)head);
+  Writer h{hb.data(), head};
+  emit_header(h, shape, ndim);
+  sink.copy(0, hb.data(), head);
+}
+// off[lo + 1 .. hi] from off[lo] and the bit lengths of elements lo .. hi-1
+// (bits[0] = element lo's)
+inline void layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                        int64_t* off) {
+  for (int64_t i = lo; i < hi; ++i) off[i + 1] = off[i] + elem_bytes_bits(bits[i - lo], n2w, exps[i], i, count);
+}
+inline void write_foot(int64_t at, const Sink& sink) {
+  uint8_t foot[3];
+  Writer f{foot, 3};
+  emit_footer(f);
+  sink.copy(at, foot, 3);
+}
+
 // Elements lo .. hi-1 (rows: their words, row lo first) at the offsets of
 // `layout`. Returns false when a row's size disagrees with its offsets (its
 // bit length was not the one the layout was made from).

@@ -236,12 +236,61 @@ int xhe_wire_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t
   return guarded([&]() -> int {
     if (!rows || !exps || !elem_off || !out || lo < 0 || hi < lo || hi > count || n2w <= 0 || n2w > 1023)
       return xhe_fail(XHE_EINVAL, "xhe_wire_rows: bad argument");
-    const int64_t pk = elem_off[count] + 3;
-    if ((framed ? xhe_zstd_raw_frame_size(pk) : pk) > cap)
+    // the rows' last byte must fit (elem_off[count] may not be known yet: the
+    // incremental layout fills the offsets range by range)
+    const int64_t end = elem_off[hi];
+    if (elem_off[lo] < 0 || end < elem_off[lo] || (framed ? xhe_zstd_raw_frame_size(end) : end) > cap)
       return xhe_fail(XHE_EOVERFLOW, "xhe_wire_rows: output buffer smaller than the layout");
     const xhe::wire::Sink sink{out, framed ? kZstdBlock : 0};
     if (!xhe::wire::write_rows(rows, exps, lo, hi, count, n2w, elem_off, sink, codec_threads()))
       return xhe_fail(XHE_EINVAL, "xhe_wire_rows: a row's bit length differs from the layout's");
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_begin(const int32_t* exps, int64_t count, int n2w, const int64_t* shape, int ndim, int framed,
+                   int64_t* elem_off, int64_t* max_len, uint8_t* out, int64_t cap) {
+  return guarded([&]() -> int {
+    if (!elem_off || !max_len || count < 0 || n2w <= 0 || n2w > 1023 || ndim < 0 || ndim > 8 ||
+        (count > 0 && !exps) || (ndim > 0 && !shape))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_begin: bad argument");
+    int64_t prod = 1;
+    for (int d = 0; d < ndim; ++d) prod *= shape[d];
+    if (prod != count) return xhe_fail(XHE_EINVAL, "xhe_wire_begin: shape does not match count");
+    const int64_t head = xhe::wire::head_bytes(shape, ndim);
+    int64_t pk = head + 3;  // every element at the largest bit length its words allow
+    for (int64_t i = 0; i < count; ++i) pk += xhe::wire::elem_bytes_bits(32 * n2w, n2w, exps[i], i, count);
+    elem_off[0] = head;
+    *max_len = framed ? xhe_zstd_raw_frame_size(pk) : pk;
+    if (!out) return XHE_OK;
+    if (*max_len > cap) return xhe_fail(XHE_EOVERFLOW, "xhe_wire_begin: output buffer too small");
+    xhe::wire::write_head(shape, ndim, xhe::wire::Sink{out, framed ? kZstdBlock : 0});
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
+                         int64_t* elem_off) {
+  return guarded([&]() -> int {
+    if (!elem_off || lo < 0 || hi < lo || hi > count || n2w <= 0 || n2w > 1023 || (hi > lo && (!bits || !exps)))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_layout_part: bad argument");
+    for (int64_t i = 0; i < hi - lo; ++i)
+      if (bits[i] < 0 || bits[i] > 32 * n2w)
+        return xhe_fail(XHE_EINVAL, "xhe_wire_layout_part: bit length out of range");
+    xhe::wire::layout_part(bits, exps, lo, hi, count, n2w, elem_off);
+    return XHE_OK;
+  });
+}
+
+int xhe_wire_finish(int64_t count, const int64_t* elem_off, int framed, uint8_t* out, int64_t cap, int64_t* out_len) {
+  return guarded([&]() -> int {
+    if (!elem_off || !out || !out_len || count < 0) return xhe_fail(XHE_EINVAL, "xhe_wire_finish: bad argument");
+    const int64_t pk = elem_off[count] + 3;
+    const int64_t need = framed ? xhe_zstd_raw_frame_size(pk) : pk;
+    *out_len = need;
+    if (need > cap) return xhe_fail(XHE_EOVERFLOW, "xhe_wire_finish: output buffer smaller than the payload");
+    xhe::wire::write_foot(elem_off[count], xhe::wire::Sink{out, framed ? kZstdBlock : 0});
+    if (framed) write_frame_headers(out, pk);
     return XHE_OK;
   });
 }

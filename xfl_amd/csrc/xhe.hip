@@ -207,6 +207,9 @@ inline uint32_t inv_2_32(uint32_t a) {  // odd a
   for (int i = 0; i < 5; ++i) x *= 2u - a * x;
   return x;
 }
+inline uint32_t shoup_const(uint32_t w, uint32_t m) {  // floor(w 2^32 / m), w < m
+  return (uint32_t)(((uint64_t)w << 32) / m);
+}
 inline uint32_t mod_small(const BigU& x, uint32_t m) {  // m = 0: mod 2^32
   if (m == 0) return x.word(0);
   uint64_t r = 0;
@@ -242,29 +245,33 @@ inline const Bases& bases() {
     }
     std::vector<uint32_t>& s = r.shared;
     s.assign(S_WORDS, 0u);
-    for (int t = 0; t < NT; ++t) {
-      const bool gB = t < 128;
-      const int ch = gB ? t : t - 128;
-      const bool isr = t == RLANE;
+    for (int slot = 0; slot < NSLOT; ++slot) {  // slot = 80 base + channel; B' channel RCH is r
+      const bool gB = slot < 80;
+      const int ch = gB ? slot : slot - 80;
+      const bool isr = !gB && ch == RCH;
       if (!(ch < RK || isr)) continue;
       const uint32_t m = isr ? 0u : (gB ? r.b[ch] : r.b2[ch]);
       if (m) {
-        s[S_M + t] = m;
-        s[S_MU + t] = (uint32_t)((1ull << 59) / m);
-        s[S_T32 + t] = (uint32_t)((1ull << 32) % m);
+        s[S_M + slot] = m;
+        s[S_MU + slot] = (uint32_t)((1ull << 59) / m);
+        s[S_T32 + slot] = (uint32_t)((1ull << 32) % m);
       }
       for (int i = 0; i < RK; ++i)  // B: |M'_j|_(m_i); B': |M_i|_(m'_j); 2^32: |M_i|_(2^32)
-        s[S_ROWS + i * NT + t] = gB ? mod_small(r.M2j[i], m) : mod_small(r.Mi[i], m);
+        s[S_ROWS + i * NSLOT + slot] = gB ? mod_small(r.M2j[i], m) : mod_small(r.Mi[i], m);
       if (gB) {
-        s[S_B + t] = mod_small(r.M2, m);                       // |M'|_(m_i)
-        s[S_C + t] = inv_mod(mod_small(r.Mi[ch], m), m);        // |M_i^-1|_(m_i)
+        s[S_B + slot] = mod_small(r.M2, m);                       // |M'|_(m_i)
+        s[S_C + slot] = inv_mod(mod_small(r.Mi[ch], m), m);        // |M_i^-1|_(m_i)
       } else if (!isr) {
         const uint64_t minv = inv_mod(mod_small(r.M, m), m);
-        s[S_B + t] = (uint32_t)minv;                                                   // |M^-1|_(m'_j)
-        s[S_C + t] = (uint32_t)(minv * inv_mod(mod_small(r.M2j[ch], m), m) % m);     // |M^-1 M'_j^-1|_(m'_j)
-        s[S_D + t] = r.M2j[ch].word(0);                         // |M'_j|_(2^32)
+        s[S_B + slot] = (uint32_t)minv;                                               // |M^-1|_(m'_j)
+        s[S_C + slot] = (uint32_t)(minv * inv_mod(mod_small(r.M2j[ch], m), m) % m);  // |M^-1 M'_j^-1|_(m'_j)
+        s[S_D + slot] = r.M2j[ch].word(0);                                            // |M'_j|_(2^32)
       } else {
-        s[S_B + t] = inv_2_32(r.M.word(0));                     // M^-1 mod 2^32
+        s[S_B + slot] = inv_2_32(r.M.word(0));  // M^-1 mod 2^32
+      }
+      if (m) {
+        s[S_BS + slot] = shoup_const(s[S_B + slot], m);
+        s[S_CS + slot] = shoup_const(s[S_C + slot], m);
       }
     }
     for (int i = 0; i < RK; ++i) {
@@ -289,23 +296,25 @@ inline std::vector<uint32_t> prime_block(const BigU& P) {
   std::vector<uint32_t> v(P_WORDS, 0u);
   const BigU MN = mod(b.M, N);
   const BigU M3 = mulmod(mulmod(MN, MN, N), MN, N);
-  for (int t = 0; t < NT; ++t) {
-    const bool gB = t < 128;
-    const int ch = gB ? t : t - 128;
-    const bool isr = t == RLANE;
+  for (int slot = 0; slot < NSLOT; ++slot) {
+    const bool gB = slot < 80;
+    const int ch = gB ? slot : slot - 80;
+    const bool isr = !gB && ch == RCH;
     if (!(ch < RK || isr)) continue;
     const uint32_t m = isr ? 0u : (gB ? b.b[ch] : b.b2[ch]);
     if (gB) {
       const uint64_t ni = inv_mod(mod_small(N, m), m), mi = inv_mod(mod_small(b.Mi[ch], m), m);
-      v[P_A + t] = (uint32_t)((m - ni * mi % m) % m);
+      v[P_A + slot] = (uint32_t)((m - ni * mi % m) % m);
     } else if (!isr) {
       const uint64_t nm = (uint64_t)mod_small(N, m) * inv_mod(mod_small(b.M, m), m) % m;
-      v[P_A + t] = (uint32_t)nm;
-      v[P_A2 + t] = (uint32_t)(nm * inv_mod(mod_small(b.M2j[ch], m), m) % m);
+      v[P_A + slot] = (uint32_t)nm;
+      v[P_A2 + slot] = (uint32_t)(nm * inv_mod(mod_small(b.M2j[ch], m), m) % m);
+      v[P_A2S + slot] = shoup_const(v[P_A2 + slot], m);
     } else {
-      v[P_A + t] = N.word(0);
+      v[P_A + slot] = N.word(0);
     }
-    v[P_M3 + t] = mod_small(M3, m);
+    if (m) v[P_AS + slot] = shoup_const(v[P_A + slot], m);
+    v[P_M3 + slot] = mod_small(M3, m);
   }
   // schedule over e = P - 1 (bits high to low)
   const BigU e = sub(P, BigU(1));
@@ -1898,9 +1907,11 @@ void raw_encrypt_impl(const xhe_key* k, const uint32_t* m, int64_t count, uint32
 // 11.3/11.8/11.9 ms for 4 lanes; 4 lanes 20-21 ms at 16 k vs 36 ms for 1
 // lane, 40 ms at 32 k vs 37 ms). $XHE_DEC_TPI (1, 4 or 16) pins one shape.
 constexpr int64_t kDecRowMax = 5120;
-// One 64-lane wave per residue (k_dec_wave, 2048-bit keys) up to kDecWaveMax
-// elements; $XHE_DEC_TPI=64 pins it.
-constexpr int64_t kDecWaveMax = 512;
+// One 256-thread block per residue (k_dec_rns, 2048-bit keys) up to
+// kDecWaveMax elements (tools/dec_shapes.py, profiles/r6: 1,024 elements
+// 5.68 ms vs 6.11 ms in 16 lanes, 1,536 8.34 vs 6.13 ms); $XHE_DEC_TPI=64
+// pins it.
+constexpr int64_t kDecWaveMax = 1024;
 constexpr int64_t kDecQuadMax = 28672;
 
 int dec_tpi_override() {
@@ -2465,6 +2476,17 @@ __global__ void k_row_bits(const uint32_t* __restrict__ w, int64_t count, int n2
 }
 
 extern "C" {
+
+#if XHE_RNS_PROBE
+// (probe builds only) k_dec_rns's cycle probe of its last launch: 16 values
+int xhe_rns_probe_read(unsigned long long* out) {
+  return guarded([&]() -> int {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rns_probe), 16 * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost));
+    return XHE_OK;
+  });
+}
+#endif
 
 int xhe_rns_constants(const uint32_t* p_words, int pw, uint32_t* shared_out, uint32_t* prime_out) {
   return guarded([&]() -> int {

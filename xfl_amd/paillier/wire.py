@@ -62,18 +62,32 @@ def encode_words(ct, exps, shape, compression=False):
 
 PIPE_MIN = 1 << 16    # device arrays from this many rows serialize through the pipeline below
 PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
-_stage = {}           # (device, n2w) -> two pinned [PIPE_CHUNK, n2w] buffers, kept for the process
+ENC_SUB = 1 << 18     # rows per encryption launch of a pipelined Paillier.encrypt (resident.encrypt_floats)
+_stage = {}           # (device, n2w) -> two pinned ([PIPE_CHUNK, n2w] words, [PIPE_CHUNK] bits), kept for the process
+_copy_streams = {}    # device -> the pipeline's copy stream
+
+
+def _copy_stream(dev):
+    import torch
+    s = _copy_streams.get(dev)
+    if s is None:
+        s = _copy_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def encode_device(d, exps, shape, compression, dev):
     """encode_words of words held in HBM (an int32 tensor [count, n2w] on
     `dev`, written by kernels on the drop-in stream - e.g. an encryption that
-    is still running): the bit length of every row is computed on the device
-    (xhe_row_bits) and comes down first, so the payload is laid out and
-    allocated before the words (xhe_wire_layout); then the rows come down in
-    chunks into a pinned double buffer, the D2H copy of chunk k + 1 running
-    while the host threads encode chunk k (xhe_wire_rows). The bytes equal
-    encode_words(download(d), ...)."""
+    is still running), chunk by chunk on a copy stream: each chunk waits only
+    for the encryption launch that writes its rows (the readiness marks
+    resident.encrypt_floats leaves on the tensor, `_xhe_ready`; else for
+    everything queued so far), then its bit lengths are computed on the device
+    (xhe_row_bits) and come down with its words into a pinned double buffer;
+    the host lays the chunk out from its bit lengths (xhe_wire_layout_part)
+    and writes its rows (xhe_wire_rows) while the next chunk is encrypted and
+    copied. The payload is allocated at the size its elements could at most
+    need (xhe_wire_begin) and cut to the real one at the end (finish, then
+    an in-place shrink). The bytes equal encode_words(download(d), ...)."""
     import torch
 
     from .. import compat
@@ -82,47 +96,66 @@ def encode_device(d, exps, shape, compression, dev):
     ex = np.ascontiguousarray(exps, dtype=np.int32).reshape(-1)
     shp = np.ascontiguousarray(shape, dtype=np.int64) if len(shape) else np.zeros(1, np.int64)
     L = nat.lib()
-    with resident._On(dev):
-        bits_d = torch.empty(count, dtype=torch.int16, device=f"cuda:{dev}")
-    nat.check(L.xhe_row_bits(resident._dp(d), count, n2w, resident._dp(bits_d), resident._sp(dev)), "row bits")
-    bits = resident.download(bits_d, np.int16)  # (waits for the kernels that write d)
-    offs = np.empty(count + 1, dtype=np.int64)
-    need = ctypes.c_int64()
-
-    def lay(framed, out, cap):
-        nat.check(L.xhe_wire_layout(_vp(bits), _vp(ex), count, n2w, _vp(shp), len(shape), int(framed), _vp(offs), out,
-                                    cap, ctypes.byref(need)), "wire layout")
-    lay(False, None, 0)
-    framed = compression and need.value >= compat.RAW_FRAME_MIN
-    if compression and not framed:
-        return encode_words(resident.download(d), ex, shape, compression=True)
-    if framed:
-        lay(True, None, 0)
-    out = nat.alloc_bytes(need.value)
-    optr = ctypes.cast(out, ctypes.c_void_p)
-    lay(framed, optr, need.value)
+    off = np.empty(count + 1, dtype=np.int64)
+    maxlen = ctypes.c_int64()
+    # (count >= PIPE_MIN: the payload is above compat.RAW_FRAME_MIN, framed when compressed)
+    framed = bool(compression)
+    assert count * 16 >= compat.RAW_FRAME_MIN
+    nat.check(L.xhe_wire_begin(_vp(ex), count, n2w, _vp(shp), len(shape), int(framed), _vp(off),
+                               ctypes.byref(maxlen), None, 0), "wire begin")
+    out = nat.alloc_bytes(maxlen.value)
+    optr = ctypes.c_void_p(ctypes.cast(out, ctypes.c_void_p).value)  # the address only (no reference)
+    nat.check(L.xhe_wire_begin(_vp(ex), count, n2w, _vp(shp), len(shape), int(framed), _vp(off),
+                               ctypes.byref(maxlen), optr, maxlen.value), "wire begin")
+    marks = getattr(d, "_xhe_ready", None)
+    if not marks or marks[-1][0] < count:
+        with resident._On(dev):
+            ev = torch.cuda.Event()
+            ev.record(resident.stream(dev))
+        marks = [(count, ev)]
     rows = min(PIPE_CHUNK, count)
-    bufs = _stage.get((dev, n2w))
-    if bufs is None or bufs[0].shape[0] < rows:
-        bufs = _stage[(dev, n2w)] = [torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    st = _stage.get((dev, n2w))
+    if st is None or st[0][0].shape[0] < rows:
+        st = _stage[(dev, n2w)] = [(torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True),
+                                    torch.empty(rows, dtype=torch.int16, pin_memory=True)) for _ in range(2)]
     chunks = [(lo, min(count, lo + PIPE_CHUNK)) for lo in range(0, count, PIPE_CHUNK)]
-    s = resident.stream(dev)
+    cs = _copy_stream(dev)
+    with torch.cuda.device(dev), torch.cuda.stream(cs):
+        bits_d = torch.empty(count, dtype=torch.int16, device=f"cuda:{dev}")
     evs = [None, None]
+    waited = [0]  # marks the copy stream already waits for
 
     def issue(k):
         lo, hi = chunks[k]
-        with resident._On(dev):
-            bufs[k % 2][:hi - lo].copy_(d[lo:hi], non_blocking=True)
+        wbuf, bbuf = st[k % 2]
+        with torch.cuda.device(dev), torch.cuda.stream(cs):
+            # every launch up to the one that writes row hi - 1 (launches on
+            # two streams may finish out of order)
+            while waited[0] < len(marks) and (waited[0] == 0 or marks[waited[0] - 1][0] < hi):
+                cs.wait_event(marks[waited[0]][1])
+                waited[0] += 1
+            nat.check(L.xhe_row_bits(resident._dp(d[lo:hi]), hi - lo, n2w, resident._dp(bits_d[lo:hi]),
+                                     ctypes.c_void_p(cs.cuda_stream)), "row bits")
+            bbuf[:hi - lo].copy_(bits_d[lo:hi], non_blocking=True)
+            wbuf[:hi - lo].copy_(d[lo:hi], non_blocking=True)
             evs[k % 2] = torch.cuda.Event()
-            evs[k % 2].record(s)
+            evs[k % 2].record(cs)
     issue(0)
     for k, (lo, hi) in enumerate(chunks):
         if k + 1 < len(chunks):
-            issue(k + 1)  # its buffer held chunk k - 1, encoded in the previous iteration
+            issue(k + 1)  # its buffers held chunk k - 1, written in the previous iteration
         evs[k % 2].synchronize()
-        nat.check(L.xhe_wire_rows(ctypes.c_void_p(bufs[k % 2].data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(offs),
-                                  int(framed), optr, need.value), "wire rows")
-    return out
+        wbuf, bbuf = st[k % 2]
+        nat.check(L.xhe_wire_layout_part(ctypes.c_void_p(bbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off)),
+                  "wire layout")
+        nat.check(L.xhe_wire_rows(ctypes.c_void_p(wbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off),
+                                  int(framed), optr, maxlen.value), "wire rows")
+    size = ctypes.c_int64()
+    nat.check(L.xhe_wire_finish(count, _vp(off), int(framed), optr, maxlen.value, ctypes.byref(size)), "wire finish")
+    del bits_d
+    box = [out]
+    del out
+    return nat.shrink_bytes(box, size.value)
 
 
 def decode(data, n2w=None):
