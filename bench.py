@@ -121,7 +121,7 @@ def pmc_traffic(win_bits, n, kernel="k_djn_pmd"):
     kernel changed between rounds; before round 4 the files were named after
     the k_djn_pow label)."""
     from xfl_amd._native import win_spec
-    for rnd, name in (("r5", kernel), ("r4", kernel), ("r3", "k_djn_pow"), ("r2", "k_djn_pow")):
+    for rnd, name in (("r6", kernel), ("r5", kernel), ("r4", kernel), ("r3", "k_djn_pow"), ("r2", "k_djn_pow")):
         if name != kernel:  # an older round's pass measured another kernel: not this one's traffic
             continue
         path = os.path.join(ROOT, "profiles", rnd, f"{name}_pmc.json")
