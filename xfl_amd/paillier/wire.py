@@ -140,16 +140,19 @@ def encode_device(d, exps, shape, compression, dev):
             wbuf[:hi - lo].copy_(d[lo:hi], non_blocking=True)
             evs[k % 2] = torch.cuda.Event()
             evs[k % 2].record(cs)
-    issue(0)
-    for k, (lo, hi) in enumerate(chunks):
-        if k + 1 < len(chunks):
-            issue(k + 1)  # its buffers held chunk k - 1, written in the previous iteration
-        evs[k % 2].synchronize()
-        wbuf, bbuf = st[k % 2]
-        nat.check(L.xhe_wire_layout_part(ctypes.c_void_p(bbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off)),
-                  "wire layout")
-        nat.check(L.xhe_wire_rows(ctypes.c_void_p(wbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off),
-                                  int(framed), optr, maxlen.value), "wire rows")
+    try:
+        issue(0)
+        for k, (lo, hi) in enumerate(chunks):
+            if k + 1 < len(chunks):
+                issue(k + 1)  # its buffers held chunk k - 1, written in the previous iteration
+            evs[k % 2].synchronize()
+            wbuf, bbuf = st[k % 2]
+            nat.check(L.xhe_wire_layout_part(ctypes.c_void_p(bbuf.data_ptr()), _vp(ex), lo, hi, count, n2w,
+                                             _vp(off)), "wire layout")
+            nat.check(L.xhe_wire_rows(ctypes.c_void_p(wbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off),
+                                      int(framed), optr, maxlen.value), "wire rows")
+    finally:
+        cs.synchronize()  # no copy still landing in the shared pinned buffers (an error mid-way)
     size = ctypes.c_int64()
     nat.check(L.xhe_wire_finish(count, _vp(off), int(framed), optr, maxlen.value, ctypes.byref(size)), "wire finish")
     del bits_d
