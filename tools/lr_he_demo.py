@@ -86,11 +86,12 @@ def _sync():
 
 
 def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, sync_phases=False, per_batch=False,
-        profile_first=False):
+        profile_first=False, profile_epoch=None):
     """Runs the HE rounds; returns a dict of phase timings and check results.
     per_batch: also a list of every batch's phase times; profile_first: a
     cProfile of the first epoch's mat-vec calls (top entries by cumulative
-    time) - the diagnosis of the first epoch's one-time costs."""
+    time) - the diagnosis of the first epoch's one-time costs;
+    profile_epoch: a cProfile of every HE phase of that (steady) epoch."""
     from xfl_amd.paillier import Paillier, PaillierContext
     xtr, ytr, _, _ = load_wdbc()
     xl, xt = xtr[:, :15], xtr[:, 15:]
@@ -117,9 +118,10 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
     epoch_tm = []
     batch_log = []
     prof = None
-    if profile_first:
+    if profile_first or profile_epoch is not None:
         import cProfile
         prof = cProfile.Profile()
+    pe = profile_epoch
     batches = checked = 0
     batch_log_prev = {}
     for ep in range(epochs):
@@ -131,6 +133,8 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
             xb_l, xb_t, yb = xl[s:s + batch], xt[s:s + batch], ytr[s:s + batch]
             pred = sigmoid(xb_l @ wl + xb_t @ wt + bias)
             resid = (yb - pred).astype(np.float32)  # label side
+            if pe is not None and ep == pe:
+                prof.enable()
             a = time.time()
             enc = Paillier.encrypt(priv, resid.astype(np.float32).flatten(), precision=7, obfuscation=True)
             if sync_phases:
@@ -144,12 +148,12 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
                              dtype=np.float32)
             noise /= 100000
             a = time.time()
-            if prof is not None and ep == 0:
+            if profile_first and ep == 0:
                 prof.enable()
             g = np.matmul(enc_t, xb_t)
             if sync_phases:
                 _sync()
-            if prof is not None and ep == 0:
+            if profile_first and ep == 0:
                 prof.disable()
             tm["matmul"] += time.time() - a
             a = time.time()
@@ -163,6 +167,8 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
             a = time.time()
             dec = Paillier.decrypt(priv, Paillier.ciphertext_from(None, wire2), dtype="float")
             tm["decrypt"] += time.time() - a
+            if pe is not None and ep == pe:
+                prof.disable()
             if check:
                 want = expected_noised_gradient(okey, resid, xb_t, noise)
                 if not np.array_equal(dec.view(np.uint32), want.view(np.uint32)):
@@ -191,7 +197,9 @@ def run(epochs=1, batch=64, check=False, key=None, max_batches=None, seed=0, syn
         import pstats
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
-        rec["first_epoch_matmul_profile"] = buf.getvalue()
+        if pe is not None:
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(30)
+        rec["first_epoch_matmul_profile" if profile_first else f"epoch{pe}_profile"] = buf.getvalue()
     if len(epoch_tm) > 1:
         # first epoch carries one-time costs (lazy code-object loads, pools);
         # later epochs are the steady state of a training run
@@ -242,9 +250,10 @@ def main():
     ap.add_argument("--cpu-batches", type=int, default=1, help="batches timed through the CPU restatement (0: skip)")
     ap.add_argument("--per-batch", action="store_true", help="every batch's phase times")
     ap.add_argument("--profile-first", action="store_true", help="cProfile of the first epoch's mat-vec calls")
+    ap.add_argument("--profile-epoch", type=int, default=None, help="cProfile of every HE phase of that epoch")
     args = ap.parse_args()
     rec = run(epochs=args.epochs, check=args.check, sync_phases=args.sync_phases, per_batch=args.per_batch,
-              profile_first=args.profile_first)
+              profile_first=args.profile_first, profile_epoch=args.profile_epoch)
     if args.cpu_batches:
         rec["cpu_restatement_s_per_batch"] = sum(cpu_batch_seconds(seed=i) for i in range(args.cpu_batches)) / \
             args.cpu_batches

@@ -179,6 +179,16 @@ def upload_async(a, dev):
         return torch.from_numpy(a).pin_memory().to(f"cuda:{dev}", non_blocking=True)
 
 
+def upload_small(a, dev, limit=1 << 20):
+    """upload_async for operands up to `limit` bytes (the host does not wait
+    for the kernels queued before the copy - in the LR step's mat-vec two
+    blocking uploads each waited for the inversion kernels ahead of them),
+    upload() for larger ones (a pinned staging copy of a big array costs more
+    than it saves)"""
+    a = np.ascontiguousarray(a)
+    return upload_async(a, dev) if a.nbytes <= limit else upload(a, dev)
+
+
 def download(t, dtype=np.uint32):
     """device tensor -> host array of `dtype` (big buffers come from the
     recycled host mappings, xfl_amd._native.empty)"""
@@ -246,7 +256,7 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
     dev = dk.device
     L = nat.lib()
     n = x.shape[0]
-    xd = upload(np.ascontiguousarray(x, dtype=np.float64), dev)
+    xd = upload_small(np.ascontiguousarray(x, dtype=np.float64), dev)
     c = max(1, min(n, CHUNK))
     from . import wire
     # large arrays: the encryption in launches of wire.ENC_SUB rows, each
@@ -369,7 +379,7 @@ def decrypt_decode(dk, c, exps):
     dev = dk.device
     L = nat.lib()
     n = c.shape[0]
-    ed = upload(np.ascontiguousarray(exps, dtype=np.int32), dev)
+    ed = upload_small(np.ascontiguousarray(exps, dtype=np.int32), dev)
     with _On(dev):
         m = torch.empty((n, dk.nw), dtype=torch.int32, device=f"cuda:{dev}")
         f64 = torch.empty(n, dtype=torch.float64, device=f"cuda:{dev}")
@@ -410,7 +420,7 @@ def powmod(dk, c, kw_, kbits, invert_first=False):
     torch = _torch()
     dev = dk.device
     kw_ = np.ascontiguousarray(kw_, dtype=np.uint32)
-    kd = upload(kw_, dev)
+    kd = upload_small(kw_, dev)
     base = invert(dk, c) if invert_first else c
     with _On(dev):
         out = torch.empty_like(c)
@@ -452,7 +462,7 @@ def multiexp(dk, bases, idx, kw_, kbits, win_bits=0):
     if iw.min() < 0 or iw.max() >= nb:
         raise ValueError("multiexp: base index out of range")
     kw_ = np.ascontiguousarray(kw_, dtype=np.uint32).reshape(ncols * nterms, -1)
-    di, dkw = upload(iw, dev), upload(kw_, dev)
+    di, dkw = upload_small(iw, dev), upload_small(kw_, dev)
     with _On(dev):
         out = torch.empty((ncols, dk.n2w), dtype=torch.int32, device=f"cuda:{dev}")
     nat.check(nat.lib().xhe_multiexp(dk.handle, _dp(bases), nb, _dp(di), _dp(dkw), kw_.shape[1], int(kbits), ncols,
