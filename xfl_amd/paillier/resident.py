@@ -256,7 +256,7 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
     dev = dk.device
     L = nat.lib()
     n = x.shape[0]
-    xd = upload_small(np.ascontiguousarray(x, dtype=np.float64), dev)
+    xd = upload(np.ascontiguousarray(x, dtype=np.float64), dev)
     c = max(1, min(n, CHUNK))
     from . import wire
     # large arrays: the encryption in launches of wire.ENC_SUB rows, each
