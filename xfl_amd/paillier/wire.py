@@ -62,7 +62,9 @@ def encode_words(ct, exps, shape, compression=False):
 
 PIPE_MIN = 1 << 16    # device arrays from this many rows serialize through the pipeline below
 PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
-ENC_SUB = 1 << 18     # rows per encryption launch of a pipelined Paillier.encrypt (resident.encrypt_floats)
+# rows per encryption launch of a pipelined Paillier.encrypt (resident.encrypt_floats);
+# $XHE_ENC_SUB overrides it (A/B measurement)
+ENC_SUB = int(__import__("os").environ.get("XHE_ENC_SUB", 1 << 18))
 _stage = {}           # (device, n2w) -> two pinned ([PIPE_CHUNK, n2w] words, [PIPE_CHUNK] bits), kept for the process
 _copy_streams = {}    # device -> the pipeline's copy stream
 
