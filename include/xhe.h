@@ -215,6 +215,10 @@ int xhe_wire_begin(const int32_t* exps, int64_t count, int n2w, const int64_t* s
                    int64_t* elem_off, int64_t* max_len, uint8_t* out, int64_t cap);
 int xhe_wire_layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, int64_t hi, int64_t count, int n2w,
                          int64_t* elem_off);
+/* layout_part from the rows' own words (rows[0] = element lo) instead of
+ * device-computed bit lengths. */
+int xhe_wire_layout_part_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count,
+                              int n2w, int64_t* elem_off);
 int xhe_wire_finish(int64_t count, const int64_t* elem_off, int framed, uint8_t* out, int64_t cap, int64_t* out_len);
 
 /* A zstd frame (RFC 8878, one frame, content size in the header) holding

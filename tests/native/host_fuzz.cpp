@@ -202,7 +202,10 @@ static void own_format(std::mt19937_64& rng) {
           xhe::wire::write_head(shape, 2, is);
           for (int64_t lo = 0; lo < count; lo += 1000) {
             const int64_t hi = std::min<int64_t>(count, lo + 1000);
-            xhe::wire::layout_part(bits.data() + lo, ex.data(), lo, hi, count, n2w, o2.data());
+            if ((lo / 1000) % 2)
+              xhe::wire::layout_part_rows(ct.data() + (size_t)lo * n2w, ex.data(), lo, hi, count, n2w, o2.data());
+            else
+              xhe::wire::layout_part(bits.data() + lo, ex.data(), lo, hi, count, n2w, o2.data());
             if (!xhe::wire::write_rows(ct.data() + (size_t)lo * n2w, ex.data(), lo, hi, count, n2w, o2.data(), is,
                                        threads))
               std::abort();

@@ -121,11 +121,14 @@ def test_incremental_layout_equals_one_pass(framed):
     nat.check(L.xhe_wire_begin(vp(ex), count, n2w, vp(shp), 1, int(framed), vp(off), ctypes.byref(mx), optr, mx.value))
     bits = np.array([0 if not r.any() else 32 * int(np.nonzero(r)[0][-1]) + int(r[np.nonzero(r)[0][-1]]).bit_length()
                      for r in ct], np.int16)
-    for lo in range(0, count, 1234):
+    for k, lo in enumerate(range(0, count, 1234)):
         hi = min(count, lo + 1234)
-        b = np.ascontiguousarray(bits[lo:hi])
-        nat.check(L.xhe_wire_layout_part(vp(b), vp(ex), lo, hi, count, n2w, vp(off)))
         rows = np.ascontiguousarray(ct[lo:hi])
+        if k % 2:  # the offsets from the rows' own words, or from device-style bit lengths
+            nat.check(L.xhe_wire_layout_part_rows(vp(rows), vp(ex), lo, hi, count, n2w, vp(off)))
+        else:
+            b = np.ascontiguousarray(bits[lo:hi])
+            nat.check(L.xhe_wire_layout_part(vp(b), vp(ex), lo, hi, count, n2w, vp(off)))
         nat.check(L.xhe_wire_rows(vp(rows), vp(ex), lo, hi, count, n2w, vp(off), int(framed), optr, mx.value))
     size = ctypes.c_int64()
     nat.check(L.xhe_wire_finish(count, vp(off), int(framed), optr, mx.value, ctypes.byref(size)))

@@ -75,6 +75,8 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_int64), _vp, ctypes.c_int64]),
     "xhe_wire_layout_part": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                             _vp]),
+    "xhe_wire_layout_part_rows": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                                 ctypes.c_int, _vp]),
     "xhe_wire_finish": (ctypes.c_int, [ctypes.c_int64, _vp, ctypes.c_int, _vp, ctypes.c_int64,
                                        ctypes.POINTER(ctypes.c_int64)]),
     "xhe_row_bits": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp]),

@@ -456,6 +456,19 @@ inline void layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, in
                         int64_t* off) {
   for (int64_t i = lo; i < hi; ++i) off[i + 1] = off[i] + elem_bytes_bits(bits[i - lo], n2w, exps[i], i, count);
 }
+// the same from the rows themselves (rows[0] = element lo): the bit lengths
+// are read off each row's top word (the words are on the host anyway when the
+// rows are written next; no device pass that would queue behind running kernels)
+inline void layout_part_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count,
+                             int n2w, int64_t* off) {
+  for (int64_t i = lo; i < hi; ++i) {
+    const uint32_t* r = rows + (size_t)(i - lo) * n2w;
+    int k = n2w - 1;
+    while (k >= 0 && r[k] == 0u) --k;
+    const int bits = k < 0 ? 0 : 32 * k + 32 - __builtin_clz(r[k]);
+    off[i + 1] = off[i] + elem_bytes_bits(bits, n2w, exps[i], i, count);
+  }
+}
 inline void write_foot(int64_t at, const Sink& sink) {
   uint8_t foot[3];
   Writer f{foot, 3};

@@ -282,6 +282,16 @@ int xhe_wire_layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, i
   });
 }
 
+int xhe_wire_layout_part_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count,
+                              int n2w, int64_t* elem_off) {
+  return guarded([&]() -> int {
+    if (!elem_off || lo < 0 || hi < lo || hi > count || n2w <= 0 || n2w > 1023 || (hi > lo && (!rows || !exps)))
+      return xhe_fail(XHE_EINVAL, "xhe_wire_layout_part_rows: bad argument");
+    xhe::wire::layout_part_rows(rows, exps, lo, hi, count, n2w, elem_off);
+    return XHE_OK;
+  });
+}
+
 int xhe_wire_finish(int64_t count, const int64_t* elem_off, int framed, uint8_t* out, int64_t cap, int64_t* out_len) {
   return guarded([&]() -> int {
     if (!elem_off || !out || !out_len || count < 0) return xhe_fail(XHE_EINVAL, "xhe_wire_finish: bad argument");

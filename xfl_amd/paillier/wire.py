@@ -65,7 +65,7 @@ PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
 # rows per encryption launch of a pipelined Paillier.encrypt (resident.encrypt_floats);
 # $XHE_ENC_SUB overrides it (A/B measurement)
 ENC_SUB = int(__import__("os").environ.get("XHE_ENC_SUB", 1 << 18))
-_stage = {}           # (device, n2w) -> two pinned ([PIPE_CHUNK, n2w] words, [PIPE_CHUNK] bits), kept for the process
+_stage = {}           # (device, n2w) -> two pinned [PIPE_CHUNK, n2w] word buffers, kept for the process
 _copy_streams = {}    # device -> the pipeline's copy stream
 
 
@@ -80,16 +80,18 @@ def _copy_stream(dev):
 def encode_device(d, exps, shape, compression, dev):
     """encode_words of words held in HBM (an int32 tensor [count, n2w] on
     `dev`, written by kernels on the drop-in stream - e.g. an encryption that
-    is still running), chunk by chunk on a copy stream: each chunk waits only
-    for the encryption launch that writes its rows (the readiness marks
-    resident.encrypt_floats leaves on the tensor, `_xhe_ready`; else for
-    everything queued so far), then its bit lengths are computed on the device
-    (xhe_row_bits) and come down with its words into a pinned double buffer;
-    the host lays the chunk out from its bit lengths (xhe_wire_layout_part)
-    and writes its rows (xhe_wire_rows) while the next chunk is encrypted and
-    copied. The payload is allocated at the size its elements could at most
-    need (xhe_wire_begin) and cut to the real one at the end (finish, then
-    an in-place shrink). The bytes equal encode_words(download(d), ...)."""
+    is still running), chunk by chunk: each chunk's D2H copy, on a copy
+    stream, waits only for the encryption launches that write its rows (the
+    readiness marks resident.encrypt_floats leaves on the tensor,
+    `_xhe_ready`; else for everything queued so far) and lands in a pinned
+    double buffer; the host lays the chunk out from the rows' own top words
+    (xhe_wire_layout_part_rows: offsets from the previous chunk's end) and
+    writes its rows (xhe_wire_rows) while the next chunk is encrypted and
+    copied. The copy stream runs copies only - a kernel there would queue
+    behind the encryption's blocks for CU slots. The payload is allocated at
+    the size its elements could at most need (xhe_wire_begin) and cut to the
+    real one at the end (finish, then an in-place shrink). The bytes equal
+    encode_words(download(d), ...)."""
     import torch
 
     from .. import compat
@@ -102,7 +104,8 @@ def encode_device(d, exps, shape, compression, dev):
     maxlen = ctypes.c_int64()
     # (count >= PIPE_MIN: the payload is above compat.RAW_FRAME_MIN, framed when compressed)
     framed = bool(compression)
-    assert count * 16 >= compat.RAW_FRAME_MIN
+    if count * 16 < compat.RAW_FRAME_MIN:
+        raise ValueError("encode_device: below the pipeline's size (use encode_words)")
     nat.check(L.xhe_wire_begin(_vp(ex), count, n2w, _vp(shp), len(shape), int(framed), _vp(off),
                                ctypes.byref(maxlen), None, 0), "wire begin")
     out = nat.alloc_bytes(maxlen.value)
@@ -117,47 +120,38 @@ def encode_device(d, exps, shape, compression, dev):
         marks = [(count, ev)]
     rows = min(PIPE_CHUNK, count)
     st = _stage.get((dev, n2w))
-    if st is None or st[0][0].shape[0] < rows:
-        st = _stage[(dev, n2w)] = [(torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True),
-                                    torch.empty(rows, dtype=torch.int16, pin_memory=True)) for _ in range(2)]
+    if st is None or st[0].shape[0] < rows:
+        st = _stage[(dev, n2w)] = [torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True) for _ in range(2)]
     chunks = [(lo, min(count, lo + PIPE_CHUNK)) for lo in range(0, count, PIPE_CHUNK)]
     cs = _copy_stream(dev)
-    with torch.cuda.device(dev), torch.cuda.stream(cs):
-        bits_d = torch.empty(count, dtype=torch.int16, device=f"cuda:{dev}")
     evs = [None, None]
     waited = [0]  # marks the copy stream already waits for
 
     def issue(k):
         lo, hi = chunks[k]
-        wbuf, bbuf = st[k % 2]
         with torch.cuda.device(dev), torch.cuda.stream(cs):
             # every launch up to the one that writes row hi - 1 (launches on
             # two streams may finish out of order)
             while waited[0] < len(marks) and (waited[0] == 0 or marks[waited[0] - 1][0] < hi):
                 cs.wait_event(marks[waited[0]][1])
                 waited[0] += 1
-            nat.check(L.xhe_row_bits(resident._dp(d[lo:hi]), hi - lo, n2w, resident._dp(bits_d[lo:hi]),
-                                     ctypes.c_void_p(cs.cuda_stream)), "row bits")
-            bbuf[:hi - lo].copy_(bits_d[lo:hi], non_blocking=True)
-            wbuf[:hi - lo].copy_(d[lo:hi], non_blocking=True)
+            st[k % 2][:hi - lo].copy_(d[lo:hi], non_blocking=True)
             evs[k % 2] = torch.cuda.Event()
             evs[k % 2].record(cs)
     try:
         issue(0)
         for k, (lo, hi) in enumerate(chunks):
             if k + 1 < len(chunks):
-                issue(k + 1)  # its buffers held chunk k - 1, written in the previous iteration
+                issue(k + 1)  # its buffer held chunk k - 1, written in the previous iteration
             evs[k % 2].synchronize()
-            wbuf, bbuf = st[k % 2]
-            nat.check(L.xhe_wire_layout_part(ctypes.c_void_p(bbuf.data_ptr()), _vp(ex), lo, hi, count, n2w,
-                                             _vp(off)), "wire layout")
-            nat.check(L.xhe_wire_rows(ctypes.c_void_p(wbuf.data_ptr()), _vp(ex), lo, hi, count, n2w, _vp(off),
-                                      int(framed), optr, maxlen.value), "wire rows")
+            rp = ctypes.c_void_p(st[k % 2].data_ptr())
+            nat.check(L.xhe_wire_layout_part_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off)), "wire layout")
+            nat.check(L.xhe_wire_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off), int(framed), optr, maxlen.value),
+                      "wire rows")
     finally:
         cs.synchronize()  # no copy still landing in the shared pinned buffers (an error mid-way)
     size = ctypes.c_int64()
     nat.check(L.xhe_wire_finish(count, _vp(off), int(framed), optr, maxlen.value, ctypes.byref(size)), "wire finish")
-    del bits_d
     box = [out]
     del out
     return nat.shrink_bytes(box, size.value)
