@@ -141,3 +141,24 @@ def test_incremental_layout_equals_one_pass(framed):
     elif not framed:
         assert got == want
     assert compat.decompress(got) == wire.encode_words(ct, ex, shape) if framed else True
+
+
+def test_shrink_bytes_in_place_and_shared():
+    """nat.shrink_bytes cuts a payload it holds the only reference to in
+    place (same prefix, no copy needed), and copies when something else still
+    refers to the object (the other reference keeps its full bytes)."""
+    b = nat.alloc_bytes(1 << 16)
+    ctypes.memmove(ctypes.cast(b, ctypes.c_void_p).value, bytes(range(256)) * 256, 1 << 16)
+    box = [b]
+    del b
+    got = nat.shrink_bytes(box, 1000)
+    assert got == (bytes(range(256)) * 4)[:1000] and box == []
+    big = nat.alloc_bytes(4096)
+    ctypes.memset(ctypes.cast(big, ctypes.c_void_p).value, 7, 4096)
+    keep = big
+    box = [big]
+    del big
+    got2 = nat.shrink_bytes(box, 100)
+    assert got2 == b"\x07" * 100 and len(keep) == 4096
+    with pytest.raises(ValueError):
+        nat.shrink_bytes([bytes(10)], 20)
