@@ -80,7 +80,10 @@ def test_pipeline_over_running_encryption_and_in_place_writes():
     x = rng.standard_normal(n).astype(np.float32)
     enc = Paillier.encrypt(ctx, x, precision=7)
     assert len(enc._st.d._xhe_ready) == -(-n // wire.ENC_SUB)
+    from xfl_amd import _native as nat
+    copies = nat.shrink_copies
     got = Paillier.serialize(enc, compression=True)
+    assert nat.shrink_copies == copies  # the payload was cut in place
     assert got == wire.encode_words(enc.words, enc.exponents, enc.shape, compression=True)
     enc2 = Paillier.encrypt(ctx, x, precision=7)
     Paillier.obfuscate(enc2[1000:2000])

@@ -158,7 +158,8 @@ def test_shrink_bytes_in_place_and_shared():
     keep = big
     box = [big]
     del big
+    copies = nat.shrink_copies
     got2 = nat.shrink_bytes(box, 100)
-    assert got2 == b"\x07" * 100 and len(keep) == 4096
+    assert got2 == b"\x07" * 100 and len(keep) == 4096 and nat.shrink_copies == copies + 1
     with pytest.raises(ValueError):
         nat.shrink_bytes([bytes(10)], 20)

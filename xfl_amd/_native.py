@@ -197,6 +197,9 @@ def _pybytes(n):
     return f(None, n)
 
 
+shrink_copies = 0  # shrink_bytes calls that had to copy (tests check the pipeline never does)
+
+
 def shrink_bytes(box, n):
     """box: a one-element list holding the only reference to a bytes object
     (from alloc_bytes); returns that object cut to its first n bytes in place
@@ -211,6 +214,8 @@ def shrink_bytes(box, n):
     if not 2 <= n < len(b):
         raise ValueError("shrink_bytes: n must be in [2, len)")
     if sys.getrefcount(b) != 2:  # b + getrefcount's argument
+        global shrink_copies
+        shrink_copies += 1
         return b[:n]
     api = ctypes.pythonapi
     api.Py_IncRef.argtypes = [ctypes.c_void_p]

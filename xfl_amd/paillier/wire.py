@@ -67,6 +67,7 @@ PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
 ENC_SUB = int(__import__("os").environ.get("XHE_ENC_SUB", 1 << 18))
 _stage = {}           # (device, n2w) -> two pinned [PIPE_CHUNK, n2w] word buffers, kept for the process
 _copy_streams = {}    # device -> the pipeline's copy stream
+_stage_lock = __import__("threading").Lock()  # one pipeline at a time uses the pinned buffers
 
 
 def _copy_stream(dev):
@@ -118,6 +119,18 @@ def encode_device(d, exps, shape, compression, dev):
             ev = torch.cuda.Event()
             ev.record(resident.stream(dev))
         marks = [(count, ev)]
+    with _stage_lock:
+        size = _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks)
+    box = [out]
+    del out  # the box holds the only reference: the cut is in place
+    return nat.shrink_bytes(box, size)
+
+
+def _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks):
+    """encode_device's chunk loop (under _stage_lock: the pinned buffers are
+    shared by every call); returns the payload's real size"""
+    import torch
+    L = nat.lib()
     rows = min(PIPE_CHUNK, count)
     st = _stage.get((dev, n2w))
     if st is None or st[0].shape[0] < rows:
@@ -152,9 +165,7 @@ def encode_device(d, exps, shape, compression, dev):
         cs.synchronize()  # no copy still landing in the shared pinned buffers (an error mid-way)
     size = ctypes.c_int64()
     nat.check(L.xhe_wire_finish(count, _vp(off), int(framed), optr, maxlen.value, ctypes.byref(size)), "wire finish")
-    box = [out]
-    del out
-    return nat.shrink_bytes(box, size.value)
+    return size.value
 
 
 def decode(data, n2w=None):
