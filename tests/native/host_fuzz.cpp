@@ -212,6 +212,11 @@ static void own_format(std::mt19937_64& rng) {
           }
           xhe::wire::write_foot(o2[count], is);
           if (o2[count] + 3 != need || o2 != offs) std::abort();
+          // one range over several threads gives the same offsets
+          std::vector<int64_t> o3((size_t)count + 1, -1);
+          o3[0] = o2[0];
+          xhe::wire::layout_part_rows(ct.data(), ex.data(), 0, count, count, n2w, o3.data(), threads);
+          if (o3 != offs) std::abort();
           if (std::memcmp(inc.data(), out.data(), (size_t)need)) std::abort();
         }
         if (count > 1) {  // a wrong bit length is refused

@@ -460,14 +460,29 @@ inline void layout_part(const int16_t* bits, const int32_t* exps, int64_t lo, in
 // are read off each row's top word (the words are on the host anyway when the
 // rows are written next; no device pass that would queue behind running kernels)
 inline void layout_part_rows(const uint32_t* rows, const int32_t* exps, int64_t lo, int64_t hi, int64_t count,
-                             int n2w, int64_t* off) {
-  for (int64_t i = lo; i < hi; ++i) {
-    const uint32_t* r = rows + (size_t)(i - lo) * n2w;
-    int k = n2w - 1;
-    while (k >= 0 && r[k] == 0u) --k;
-    const int bits = k < 0 ? 0 : 32 * k + 32 - __builtin_clz(r[k]);
-    off[i + 1] = off[i] + elem_bytes_bits(bits, n2w, exps[i], i, count);
-  }
+                             int n2w, int64_t* off, int threads = 1) {
+  const int64_t n = hi - lo;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / 4096));
+  std::vector<int64_t> tot((size_t)T + 1, 0);
+  run_parallel(T, [&](int t) {  // per element: its size into off[i + 1], exclusive prefix within the part
+    const int64_t a = lo + n * t / T, b = lo + n * (t + 1) / T;
+    int64_t acc = 0;
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t* r = rows + (size_t)(i - lo) * n2w;
+      int k = n2w - 1;
+      while (k >= 0 && r[k] == 0u) --k;
+      const int bits = k < 0 ? 0 : 32 * k + 32 - __builtin_clz(r[k]);
+      acc += elem_bytes_bits(bits, n2w, exps[i], i, count);
+      off[i + 1] = acc;
+    }
+    tot[(size_t)t + 1] = acc;
+  });
+  tot[0] = off[lo];
+  for (int t = 0; t < T; ++t) tot[(size_t)t + 1] += tot[(size_t)t];
+  run_parallel(T, [&](int t) {
+    const int64_t a = lo + n * t / T, b = lo + n * (t + 1) / T;
+    for (int64_t i = a; i < b; ++i) off[i + 1] += tot[(size_t)t];
+  });
 }
 inline void write_foot(int64_t at, const Sink& sink) {
   uint8_t foot[3];

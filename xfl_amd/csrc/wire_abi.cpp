@@ -287,7 +287,7 @@ int xhe_wire_layout_part_rows(const uint32_t* rows, const int32_t* exps, int64_t
   return guarded([&]() -> int {
     if (!elem_off || lo < 0 || hi < lo || hi > count || n2w <= 0 || n2w > 1023 || (hi > lo && (!rows || !exps)))
       return xhe_fail(XHE_EINVAL, "xhe_wire_layout_part_rows: bad argument");
-    xhe::wire::layout_part_rows(rows, exps, lo, hi, count, n2w, elem_off);
+    xhe::wire::layout_part_rows(rows, exps, lo, hi, count, n2w, elem_off, codec_threads());
     return XHE_OK;
   });
 }
