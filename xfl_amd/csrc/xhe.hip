@@ -11,6 +11,7 @@
 #include <mutex>
 #include <atomic>
 #include <stdexcept>
+#include <unordered_map>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -986,6 +987,29 @@ struct WsCache {
 };
 thread_local WsCache* t_ws = nullptr;
 
+// Outside a host pipeline, a workspace freed on stream s is kept on s's free
+// list for the next call on s (stream order makes that reuse safe) instead of
+// going back to the pool: a pipelined Paillier.encrypt alternates its pieces
+// between two streams, and a request on one stream for memory the other had
+// just freed made hipMallocAsync hold the host until that stream drained
+// (the launches serialised behind each other). At most kStreamWsKeep bytes
+// are kept per stream; a block is reused for requests of at least half its
+// size.
+constexpr size_t kStreamWsKeep = (size_t)2 << 30;
+struct StreamWs {
+  struct Blk {
+    void* p;
+    size_t bytes;
+  };
+  std::mutex mu;
+  std::unordered_map<hipStream_t, std::vector<Blk>> free;  // oldest first
+  std::unordered_map<void*, size_t> size;                  // blocks handed out
+};
+StreamWs& stream_ws() {
+  static StreamWs* w = new StreamWs();  // process lifetime (no teardown order with the runtime)
+  return *w;
+}
+
 void ws_alloc(void** p, size_t bytes, hipStream_t s) {
   if (t_ws) {
     for (auto& b : t_ws->blk)
@@ -998,7 +1022,27 @@ void ws_alloc(void** p, size_t bytes, hipStream_t s) {
     t_ws->blk.push_back({*p, bytes, true});
     return;
   }
+  StreamWs& w = stream_ws();
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    auto it = w.free.find(s);
+    if (it != w.free.end()) {
+      std::vector<StreamWs::Blk>& v = it->second;
+      size_t best = v.size();
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].bytes >= bytes && v[i].bytes / 2 <= bytes && (best == v.size() || v[i].bytes < v[best].bytes))
+          best = i;
+      if (best < v.size()) {
+        *p = v[best].p;
+        w.size[*p] = v[best].bytes;
+        v.erase(v.begin() + (ptrdiff_t)best);
+        return;
+      }
+    }
+  }
   HIPCHK(hipMallocAsync(p, bytes, s));
+  std::lock_guard<std::mutex> g(w.mu);
+  w.size[*p] = bytes;
 }
 
 void ws_free(void* p, hipStream_t s) {
@@ -1008,7 +1052,27 @@ void ws_free(void* p, hipStream_t s) {
         b.used = false;
         return;
       }
-  HIPCHK(hipFreeAsync(p, s));
+  StreamWs& w = stream_ws();
+  std::vector<void*> drop;
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    auto it = w.size.find(p);
+    if (it == w.size.end()) {
+      drop.push_back(p);  // not one of ours (allocated inside a host pipeline's cache, never here)
+    } else {
+      std::vector<StreamWs::Blk>& v = w.free[s];
+      v.push_back({p, it->second});
+      w.size.erase(it);
+      size_t total = 0;
+      for (const auto& b : v) total += b.bytes;
+      while (total > kStreamWsKeep && !v.empty()) {
+        total -= v.front().bytes;
+        drop.push_back(v.front().p);
+        v.erase(v.begin());
+      }
+    }
+  }
+  for (void* q : drop) HIPCHK(hipFreeAsync(q, s));
 }
 
 constexpr int64_t kChunk = 1 << 20;  // elements per launch chunk (bounds workspace)

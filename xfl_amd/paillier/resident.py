@@ -245,6 +245,7 @@ def _seed():
     return s()
 
 
+ENC_STREAMS = int(os.environ.get("XHE_ENC_STREAMS", 2))  # streams the pieces of a pipelined encryption alternate on
 CHUNK = 1 << 20  # elements per encode/draw/encrypt pass: bounds the m + draw temporaries (~400 MB at 2048 bits)
 
 
@@ -271,11 +272,11 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
         es = torch.empty((2, n), dtype=torch.int32, device=f"cuda:{dev}")
         m = torch.empty((c, dk.nw), dtype=torch.int32, device=f"cuda:{dev}")
         rnds = [torch.empty((min(sub, c), dk.rand_words), dtype=torch.int32, device=f"cuda:{dev}")
-                for _ in range(2 if sub < c else 1)] if obfuscation else [None, None]
+                for _ in range(2 if sub < c and ENC_STREAMS > 1 else 1)] if obfuscation else [None, None]
     prec = -1 if precision is None else int(precision)
     has_max = max_exponent is not None
     main = stream(dev)
-    streams = [main, aux_stream(dev)] if sub < c else [main]
+    streams = [main, aux_stream(dev)] if sub < c and ENC_STREAMS > 1 else [main]
     es_h = None
     marks = []
     j = 0

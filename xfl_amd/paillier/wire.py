@@ -67,7 +67,8 @@ PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
 ENC_SUB = int(__import__("os").environ.get("XHE_ENC_SUB", 1 << 18))
 _stage = {}           # (device, n2w) -> two pinned [PIPE_CHUNK, n2w] word buffers, kept for the process
 _copy_streams = {}    # device -> the pipeline's copy stream
-_stage_lock = __import__("threading").Lock()  # one pipeline at a time uses the pinned buffers
+_stage_lock = __import__("threading").Lock()
+_TRACE = __import__("os").environ.get("XHE_PIPE_TRACE", "0") not in ("", "0")  # per-chunk timings on stderr  # one pipeline at a time uses the pinned buffers
 
 
 def _copy_stream(dev):
@@ -151,16 +152,26 @@ def _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks):
             st[k % 2][:hi - lo].copy_(d[lo:hi], non_blocking=True)
             evs[k % 2] = torch.cuda.Event()
             evs[k % 2].record(cs)
+    trace = _TRACE and []
+    t0 = __import__("time").perf_counter()
     try:
         issue(0)
         for k, (lo, hi) in enumerate(chunks):
             if k + 1 < len(chunks):
                 issue(k + 1)  # its buffer held chunk k - 1, written in the previous iteration
             evs[k % 2].synchronize()
+            t1 = __import__("time").perf_counter()
             rp = ctypes.c_void_p(st[k % 2].data_ptr())
             nat.check(L.xhe_wire_layout_part_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off)), "wire layout")
+            t2 = __import__("time").perf_counter()
             nat.check(L.xhe_wire_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off), int(framed), optr, maxlen.value),
                       "wire rows")
+            if trace is not False:
+                t3 = __import__("time").perf_counter()
+                trace.append((k, round((t1 - t0) * 1e3, 2), round((t2 - t1) * 1e3, 2), round((t3 - t2) * 1e3, 2)))
+        if trace:
+            import sys
+            print("pipeline (chunk, ready_ms, layout_ms, rows_ms):", trace, file=sys.stderr, flush=True)
     finally:
         cs.synchronize()  # no copy still landing in the shared pinned buffers (an error mid-way)
     size = ctypes.c_int64()
