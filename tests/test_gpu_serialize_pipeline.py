@@ -79,7 +79,7 @@ def test_pipeline_over_running_encryption_and_in_place_writes():
     n = 2 * wire.ENC_SUB + 3 * wire.PIPE_CHUNK + 77
     x = rng.standard_normal(n).astype(np.float32)
     enc = Paillier.encrypt(ctx, x, precision=7)
-    assert len(enc._st.d._xhe_ready) == -(-n // wire.ENC_SUB)
+    assert len(enc._st.d._xhe_ready) == -(-n // wire.ENC_SUB) and enc._st.d._xhe_bits.shape == (n,)
     from xfl_amd import _native as nat
     copies = nat.shrink_copies
     got = Paillier.serialize(enc, compression=True)
@@ -87,7 +87,7 @@ def test_pipeline_over_running_encryption_and_in_place_writes():
     assert got == wire.encode_words(enc.words, enc.exponents, enc.shape, compression=True)
     enc2 = Paillier.encrypt(ctx, x, precision=7)
     Paillier.obfuscate(enc2[1000:2000])
-    assert not hasattr(enc2._st.d, "_xhe_ready")
+    assert not hasattr(enc2._st.d, "_xhe_ready") and not hasattr(enc2._st.d, "_xhe_bits")
     enc2._st.h = None
     got2 = Paillier.serialize(enc2, compression=False)
     assert got2 == wire.encode_words(enc2.words, enc2.exponents, enc2.shape)

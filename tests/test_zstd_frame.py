@@ -163,3 +163,22 @@ def test_shrink_bytes_in_place_and_shared():
     assert got2 == b"\x07" * 100 and len(keep) == 4096 and nat.shrink_copies == copies + 1
     with pytest.raises(ValueError):
         nat.shrink_bytes([bytes(10)], 20)
+
+
+@pytest.mark.parametrize("count", [1, 2, 999, 1000, 1001, 2000, 5003])
+def test_wire_begin_max_len_is_the_full_width_payload(count):
+    """xhe_wire_begin's largest payload (closed form) is exactly the pickle of
+    the same exponents with every value at n2w full words."""
+    from xfl_amd.paillier import wire
+    rng = np.random.default_rng(count)
+    n2w = 128
+    ex = rng.integers(-400, 700, count).astype(np.int32)
+    full = np.full((count, n2w), 0xFFFFFFFF, np.uint32)
+    want = len(wire.encode_words(full, ex, (count,)))
+    L = nat.lib()
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    off = np.empty(count + 1, np.int64)
+    mx = ctypes.c_int64()
+    shp = np.array([count], np.int64)
+    nat.check(L.xhe_wire_begin(vp(ex), count, n2w, vp(shp), 1, 0, vp(off), ctypes.byref(mx), None, 0))
+    assert mx.value == want

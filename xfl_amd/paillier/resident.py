@@ -271,6 +271,7 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
         ct = torch.empty((n, dk.n2w), dtype=torch.int32, device=f"cuda:{dev}")
         es = torch.empty((2, n), dtype=torch.int32, device=f"cuda:{dev}")
         m = torch.empty((c, dk.nw), dtype=torch.int32, device=f"cuda:{dev}")
+        bits = torch.empty(n, dtype=torch.int16, device=f"cuda:{dev}") if n >= wire.PIPE_MIN else None
         rnds = [torch.empty((min(sub, c), dk.rand_words), dtype=torch.int32, device=f"cuda:{dev}")
                 for _ in range(2 if sub < c and ENC_STREAMS > 1 else 1)] if obfuscation else [None, None]
     prec = -1 if precision is None else int(precision)
@@ -308,6 +309,8 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
                 seed, nonce = _seed()
                 nat.check(L.xhe_rand(dk.handle, seed, nonce, ks, _dp(rnd), None, sp), "rand")
             nat.check(L.xhe_encrypt(dk.handle, _dp(m[so:]), _dp(rnd), ks, _dp(ct[lo + so:]), sp), "encrypt")
+            if bits is not None:  # the piece's bit lengths for the serializer's layout, behind the piece
+                nat.check(L.xhe_row_bits(_dp(ct[lo + so:]), ks, dk.n2w, _dp(bits[lo + so:]), sp), "row bits")
             if sub < c:
                 with _On(dev):
                     ev = torch.cuda.Event()
@@ -321,6 +324,8 @@ def encrypt_floats(dk, x, precision, max_exponent, obfuscation):
                 main.wait_event(done)
     if marks:
         ct._xhe_ready = marks
+    if bits is not None:
+        ct._xhe_bits = bits
     if es_h is None:
         es_h = download(es, np.int32)
     return ct, es_h[0].copy(), es_h[1].copy()
@@ -524,9 +529,10 @@ def put_rows(c, idx, rows):
         if tuple(rows.shape) != (idx.shape[0],) + tuple(c.shape[1:]) or rows.dtype != c.dtype:
             raise ValueError(f"put_rows: rows {tuple(rows.shape)} {rows.dtype} for {idx.shape[0]} rows of {tuple(c.shape)} "
                              f"{c.dtype}")
-        for t in (c, c._base):  # rows change: an encryption's readiness marks no longer describe them
-            if t is not None and "_xhe_ready" in t.__dict__:
-                del t._xhe_ready
+        for t in (c, c._base):  # rows change: an encryption's readiness marks and bit lengths no longer describe them
+            if t is not None:
+                t.__dict__.pop("_xhe_ready", None)
+                t.__dict__.pop("_xhe_bits", None)
         ii = upload_async(idx, dev)
         with _On(dev):  # a copy made on the drop-in stream, ordered before the scatter that reads it
             src = rows.contiguous()

@@ -65,7 +65,7 @@ PIPE_CHUNK = 1 << 17  # rows per D2H chunk (64 MB at 2048 bits)
 # rows per encryption launch of a pipelined Paillier.encrypt (resident.encrypt_floats);
 # $XHE_ENC_SUB overrides it (A/B measurement)
 ENC_SUB = int(__import__("os").environ.get("XHE_ENC_SUB", 1 << 18))
-_stage = {}           # (device, n2w) -> two pinned [PIPE_CHUNK, n2w] word buffers, kept for the process
+_stage = {}           # (device, n2w) -> two pinned ([PIPE_CHUNK, n2w] words, [PIPE_CHUNK] bits), kept for the process
 _copy_streams = {}    # device -> the pipeline's copy stream
 _stage_lock = __import__("threading").Lock()
 _TRACE = __import__("os").environ.get("XHE_PIPE_TRACE", "0") not in ("", "0")  # per-chunk timings on stderr  # one pipeline at a time uses the pinned buffers
@@ -134,8 +134,14 @@ def _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks):
     L = nat.lib()
     rows = min(PIPE_CHUNK, count)
     st = _stage.get((dev, n2w))
-    if st is None or st[0].shape[0] < rows:
-        st = _stage[(dev, n2w)] = [torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    if st is None or st[0][0].shape[0] < rows:
+        st = _stage[(dev, n2w)] = [(torch.empty((rows, n2w), dtype=torch.int32, pin_memory=True),
+                                    torch.empty(rows, dtype=torch.int16, pin_memory=True)) for _ in range(2)]
+    # the bit lengths the encryption computed behind each piece (else the host
+    # reads them off the rows' top words)
+    bits_d = getattr(d, "_xhe_bits", None)
+    if bits_d is not None and bits_d.shape[0] != count:
+        bits_d = None
     chunks = [(lo, min(count, lo + PIPE_CHUNK)) for lo in range(0, count, PIPE_CHUNK)]
     cs = _copy_stream(dev)
     evs = [None, None]
@@ -149,7 +155,9 @@ def _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks):
             while waited[0] < len(marks) and (waited[0] == 0 or marks[waited[0] - 1][0] < hi):
                 cs.wait_event(marks[waited[0]][1])
                 waited[0] += 1
-            st[k % 2][:hi - lo].copy_(d[lo:hi], non_blocking=True)
+            st[k % 2][0][:hi - lo].copy_(d[lo:hi], non_blocking=True)
+            if bits_d is not None:
+                st[k % 2][1][:hi - lo].copy_(bits_d[lo:hi], non_blocking=True)
             evs[k % 2] = torch.cuda.Event()
             evs[k % 2].record(cs)
     trace = _TRACE and []
@@ -161,8 +169,12 @@ def _pipeline(d, ex, count, n2w, dev, framed, off, maxlen, optr, marks):
                 issue(k + 1)  # its buffer held chunk k - 1, written in the previous iteration
             evs[k % 2].synchronize()
             t1 = __import__("time").perf_counter()
-            rp = ctypes.c_void_p(st[k % 2].data_ptr())
-            nat.check(L.xhe_wire_layout_part_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off)), "wire layout")
+            rp = ctypes.c_void_p(st[k % 2][0].data_ptr())
+            if bits_d is not None:
+                nat.check(L.xhe_wire_layout_part(ctypes.c_void_p(st[k % 2][1].data_ptr()), _vp(ex), lo, hi, count,
+                                                 n2w, _vp(off)), "wire layout")
+            else:
+                nat.check(L.xhe_wire_layout_part_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off)), "wire layout")
             t2 = __import__("time").perf_counter()
             nat.check(L.xhe_wire_rows(rp, _vp(ex), lo, hi, count, n2w, _vp(off), int(framed), optr, maxlen.value),
                       "wire rows")
