@@ -32,14 +32,18 @@ namespace bar {
 constexpr int W = 27;
 constexpr uint32_t MASK = (1u << W) - 1u;
 constexpr int S = 152;          // limbs of n^2 at 2048-bit keys
-constexpr int G = 8;            // lanes per element
+#ifndef XHE_BAR_G
+#define XHE_BAR_G 8
+#endif
+constexpr int G = XHE_BAR_G;    // lanes per element (8; 4 for A/B: 16-column rounds)
+static_assert(G == 8 || G == 4, "8 or 4 lanes per element");
 constexpr int RCOLS = 4 * G;    // columns per round
 constexpr int YOFF = 4 * G + 7; // y-role rows: limb j at [YOFF + j]; >= 4G + 6 zeros in front, = 3 mod 4
 constexpr int YLEN = (YOFF + (S + 1) + 4 * G + 3 + 3) & ~3;  // ... and >= 4G + 2 zeros behind (LY <= S + 1)
 constexpr int XLEN = 160;       // x-role rows: limb i at [i], zeros to XLEN (LX <= S + 1, + 7 for the last pair)
 constexpr int XB = 0, YB = XLEN;
 constexpr int STRIDE = 400;     // words per element (= 16 mod 64: the elements of a b128 lane group spread over the banks)
-constexpr int TPB = 256;        // threads per block
+constexpr int TPB = 32 * G;     // threads per block (32 elements: the LDS of three blocks per CU)
 constexpr int EPB = TPB / G;    // elements per block
 constexpr int LDS_WORDS = EPB * STRIDE + 2 * YLEN;  // + the shared mu and N rows
 static_assert(XB + XLEN <= YB && YB + YLEN <= STRIDE, "element rows overlap");
@@ -64,7 +68,7 @@ XHE_DEV uint64_t prev_lane64(uint64_t v) {
 XHE_DEV uint64_t last_lane64(uint64_t v) {
   return (uint64_t)last_lane((uint32_t)v) | ((uint64_t)last_lane((uint32_t)(v >> 32)) << 32);
 }
-constexpr uint64_t TOPS = 0x8080808080808080ull;  // the last lane of every 8-lane group
+constexpr uint64_t TOPS = G == 8 ? 0x8080808080808080ull : 0x8888888888888888ull;  // the last lane of every group
 
 // acc[k] += x_ii w[k - ii + 3] for ii, k < 4 (w[t] = y_{c-i0-3+t} of a block
 // of 4 terms i0 .. i0+3): 16 mads in one statement (a separate asm per mad
@@ -220,7 +224,7 @@ XHE_DEV uint32_t sub_round(const uint32_t (&a)[4], const uint32_t (&b)[4], uint3
 
 // c = a * b mod n^2 for 2048-bit keys, equal exponents (eout = min(ea, eb)).
 // mu: floor(2^(27*304) / n^2) as 153 limbs of 27 bits (KeyDev::n2_mu).
-__global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const uint32_t* __restrict__ a,
+__global__ void __launch_bounds__(bar::TPB, bar::G == 8 ? 3 : 2) k_add_barrett(KeyDev key, const uint32_t* __restrict__ a,
                                                           const int32_t* __restrict__ ea,
                                                           const uint32_t* __restrict__ bw,
                                                           const int32_t* __restrict__ eb, int64_t count,
@@ -250,6 +254,11 @@ __global__ void __launch_bounds__(bar::TPB, 3) k_add_barrett(KeyDev key, const u
     uint32_t* dst = half ? yr + YOFF : xr;
 #pragma unroll
     for (int j = 0; j < M4::L; ++j) dst[(g & 3) * M4::L + j] = b[j];
+    if constexpr (G == 4) {  // one 4-lane group loads both operands
+      M.load_words(b, bw + (size_t)e * key.n2w, key.n2w);
+#pragma unroll
+      for (int j = 0; j < M4::L; ++j) yr[YOFF + g * M4::L + j] = b[j];
+    }
     for (int j = g; j < XLEN - S; j += G) xr[S + j] = 0u;
     for (int j = g; j < YOFF; j += G) yr[j] = 0u;
     for (int j = YOFF + S + g; j < YLEN; j += G) yr[j] = 0u;
